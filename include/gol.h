@@ -1,0 +1,154 @@
+/*
+ * gol.h -- C ABI of the MI355X Game of Life engine (libgol.so).
+ *
+ * Drop-in boundary for the hot path of krutovsky-danya/mpi-game-of-life,
+ * Parallel_Life_MPI.cpp.  The reference has no plugin API: its hot path is
+ * `void updateGrid()` (:37-54, with countNeighbours :16-35) mutating the
+ * process globals `grid`/`nextGrid` (:13), driven by the loop in main
+ * (:215-221) together with `exchangeGridData` (:104-145), and fed/drained by
+ * readGridFromFile (:56-102) and writeDataToFile (:147-188).  This header
+ * replaces main's lines :211-231 (read -> epochs x {update, exchange, barrier}
+ * -> write) with an engine handle; each entry point names the reference code
+ * it stands in for.
+ *
+ * Conventions
+ *  - Cells: bit-packed, 64 per uint64, row-major; bit j of word q is column 64q+j.
+ *    Columns >= w are kept 0.  Outside the field every cell is dead
+ *    (Parallel_Life_MPI.cpp:21-27).
+ *  - Rule: a (birth, survive) pair of 9-bit masks, bit n <=> n live neighbours.
+ *    The reference's *effective* rule is birth=0, survive=1<<2 ("B/S2"): the
+ *    `count == 3` store at :44-46 is always overwritten by :47-50.
+ *  - Ownership: the caller owns every host buffer; the engine owns all device
+ *    memory, its HIP stream and its RCCL communicator.
+ *  - Errors: every call returns gol_status; it never aborts.  gol_last_error()
+ *    gives a thread-local message for the last failure.
+ *  - Threading: a handle is not thread-safe; use it from one host thread.
+ */
+#ifndef GOL_H
+#define GOL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum gol_status {
+    GOL_OK = 0,
+    GOL_EINVAL = 1, /* bad argument (sizes, masks, lengths, malformed ASCII) */
+    GOL_ENOMEM = 2, /* device or host allocation failed */
+    GOL_EHIP = 3,   /* HIP runtime error */
+    GOL_ERCCL = 4,  /* RCCL error */
+    GOL_EIO = 5,    /* file I/O error (CLI helpers) */
+    GOL_ESTATE = 6  /* call not valid in the engine's current state */
+} gol_status;
+
+typedef enum gol_semantics {
+    /* The reference's intended semantics == its `mpirun -np 1` output: one field
+     * evolving with a dead border. */
+    GOL_SEM_GLOBAL = 0,
+    /* The reference's actual `mpirun -np P` output: its halo exchange receives
+     * into copies (:110-111, :126-127) and has no effect, so each rank's
+     * extended stripe (:70-81) evolves alone and the output keeps each rank's
+     * own rows (:149-175).  P = gol_config.ref_ranks. */
+    GOL_SEM_REF_STRIPES = 1
+} gol_semantics;
+
+/* Reference-effective rule and Conway's rule as (birth, survive) masks. */
+#define GOL_REF_BIRTH 0u
+#define GOL_REF_SURVIVE (1u << 2)
+#define GOL_CONWAY_BIRTH (1u << 3)
+#define GOL_CONWAY_SURVIVE ((1u << 2) | (1u << 3))
+
+typedef struct gol_config {
+    uint32_t birth_mask;   /* 9-bit */
+    uint32_t survive_mask; /* 9-bit */
+    int32_t device;        /* HIP device ordinal; -1 = current device */
+    uint32_t semantics;    /* gol_semantics */
+    uint32_t ref_ranks;    /* P for GOL_SEM_REF_STRIPES (must satisfy h >= P) */
+    uint32_t tb_depth;     /* generations fused per kernel launch (temporal
+                              blocking); 0 = auto; allowed 1,2,4,8,16 */
+    uint32_t halo_depth;   /* multi-rank: halo rows exchanged per round
+                              (= generations between exchanges); 0 = auto */
+    uint32_t rows_per_wave;/* rows each wavefront streams per launch; 0 = auto */
+    uint32_t reserved[4];
+} gol_config;
+
+typedef struct gol_engine gol_engine;
+
+typedef struct gol_timing {
+    uint64_t launches;     /* stencil kernel launches timed */
+    double kernel_ms;      /* sum of their HIP-event durations */
+    double cell_gens;      /* cell-generations those launches produced (own rows) */
+    double cell_gens_computed; /* including redundant halo/overlap work */
+} gol_timing;
+
+/* Defaults: reference-effective rule, GLOBAL semantics, auto tuning. */
+void gol_config_init(gol_config* cfg);
+
+/* Replaces the allocation in readGridFromFile (:88-89).  h rows x w columns. */
+gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine** out);
+
+/* Replaces readGridFromFile's parse (:91-99): buf holds the data.txt bytes,
+ * h lines of exactly w cell bytes followed by '\n' (len == h*(w+1)); a cell is
+ * alive iff its byte is '1'.  A rank engine (gol_create_rank) takes only its
+ * own rows: len == rows*(w+1). */
+gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len);
+
+/* Replaces writeDataToFile's serialisation (:157-164): writes '0'/'1' bytes and
+ * '\n' per row, len == h*(w+1) (own rows for a rank engine). */
+gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len);
+
+/* Packed transfer; row_stride_words >= ceil(w/64).  Rank engines: own rows. */
+gol_status gol_load_packed(gol_engine* e, const uint64_t* words, uint64_t row_stride_words);
+gol_status gol_store_packed(gol_engine* e, uint64_t* words, uint64_t row_stride_words);
+
+/* Synthetic p = 0.5 field generated on the device: word (r, q) =
+ * splitmix64(seed, r*ceil(w/64)+q) masked to w (identical on the CPU oracle). */
+gol_status gol_init_random(gol_engine* e, uint64_t seed);
+
+/* Replaces the epoch loop (:215-221): advances `generations` generations
+ * (including the halo exchange of a rank engine).  Returns after the work is
+ * enqueued; gol_sync() waits for it. */
+gol_status gol_step(gol_engine* e, uint64_t generations);
+gol_status gol_sync(gol_engine* e);
+
+/* Live-cell count and an order-independent 64-bit hash of the field
+ * (sum over words of splitmix64(word ^ splitmix64(0, r*ceil(w/64)+q))).
+ * Rank engines return the partial sums of their own rows (add them up). */
+gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash);
+
+void gol_destroy(gol_engine* e);
+const char* gol_last_error(void);
+
+/* Per-launch HIP-event timing of the stencil kernel, on the engine's stream. */
+gol_status gol_set_timing(gol_engine* e, int enable);
+gol_status gol_get_timing(gol_engine* e, gol_timing* out);
+gol_status gol_reset_timing(gol_engine* e);
+
+/* Engine geometry as chosen (for tools / tests). */
+gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0,
+                    uint64_t* rows, uint32_t* tb_depth, uint32_t* halo_depth);
+
+/* ---- Multi-GPU, one process per GPU (replaces the MPI stripes :70-81 and the
+ * halo exchange :104-145 with RCCL send/recv over xGMI) ---- */
+
+/* Rows of global stripe `rank` of `nranks`: contiguous, ceil-balanced.
+ * Host-only; needs no GPU. */
+gol_status gol_rank_rows(uint64_t h, int nranks, int rank, uint64_t* row0, uint64_t* rows);
+
+/* Generate an RCCL unique id on one rank; broadcast its 128 bytes to the
+ * others by any means (torch.distributed, a file, MPI). */
+gol_status gol_comm_unique_id(uint8_t id[128]);
+
+/* Engine for stripe `rank` of `nranks` of an h x w GLOBAL field; all ranks call
+ * it collectively with the same id.  cfg->semantics must be GLOBAL. */
+gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int rank,
+                           int nranks, const uint8_t id[128], gol_engine** out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GOL_H */

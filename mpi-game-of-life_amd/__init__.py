@@ -1,0 +1,238 @@
+"""Python binding of libgol.so (include/gol.h) -- the MI355X Game of Life engine.
+
+Thin ctypes layer used by bench.py, the tests and __graft_entry__: no compute
+happens here.  Every call goes to the C ABI, whose kernels run on the GPU; there
+is no CPU fallback.  Loading fails loudly (GolError) if libgol.so is missing.
+
+The directory name is not a Python identifier, so load it with `load_package()`
+from __graft_entry__.py, or importlib with an explicit path.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgol.so")
+CLI_PATH = os.path.join(HERE, "gol")
+
+GOL_OK, GOL_EINVAL, GOL_ENOMEM, GOL_EHIP, GOL_ERCCL, GOL_EIO, GOL_ESTATE = range(7)
+SEM_GLOBAL, SEM_REF_STRIPES = 0, 1
+
+# (birth, survive) masks; bit n <=> n live neighbours
+REF_RULE = (0, 1 << 2)  # effective rule of Parallel_Life_MPI.cpp:44-50 ("B/S2")
+CONWAY = (1 << 3, (1 << 2) | (1 << 3))  # B3/S23
+
+# Every symbol include/gol.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "gol_config_init", "gol_create", "gol_load_ascii", "gol_store_ascii",
+    "gol_load_packed", "gol_store_packed", "gol_init_random", "gol_step", "gol_sync",
+    "gol_digest", "gol_destroy", "gol_last_error", "gol_set_timing", "gol_get_timing",
+    "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
+    "gol_create_rank",
+]
+
+
+class GolError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"gol status {status}: {msg}")
+        self.status = status
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("birth_mask", ctypes.c_uint32),
+        ("survive_mask", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("semantics", ctypes.c_uint32),
+        ("ref_ranks", ctypes.c_uint32),
+        ("tb_depth", ctypes.c_uint32),
+        ("halo_depth", ctypes.c_uint32),
+        ("rows_per_wave", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 4),
+    ]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [
+        ("launches", ctypes.c_uint64),
+        ("kernel_ms", ctypes.c_double),
+        ("cell_gens", ctypes.c_double),
+        ("cell_gens_computed", ctypes.c_double),
+    ]
+
+
+def build(force=False):
+    """Compile libgol.so and the CLI in-tree (hipcc --offload-arch=gfx950)."""
+    args = ["make", "-s", "-C", HERE, "-j4"]
+    if force:
+        subprocess.run(["make", "-s", "-C", HERE, "clean"], check=True)
+    subprocess.run(args, check=True)
+
+
+_lib = None
+
+
+def lib():
+    """Load libgol.so (torch first, so one HIP runtime serves the process)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GolError(-1, f"{LIB_PATH} not built; run __graft_entry__.build()")
+    try:  # share torch's HIP runtime when torch is present (same SONAME)
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    L.gol_config_init.argtypes = [ctypes.POINTER(Config)]
+    L.gol_config_init.restype = None
+    L.gol_create.argtypes = [u64, u64, ctypes.POINTER(Config), ctypes.POINTER(vp)]
+    L.gol_create_rank.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32, ctypes.c_char_p,
+                                  ctypes.POINTER(vp)]
+    L.gol_load_ascii.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
+    L.gol_store_ascii.argtypes = [vp, vp, ctypes.c_size_t]
+    L.gol_load_packed.argtypes = [vp, vp, u64]
+    L.gol_store_packed.argtypes = [vp, vp, u64]
+    L.gol_init_random.argtypes = [vp, u64]
+    L.gol_step.argtypes = [vp, u64]
+    L.gol_sync.argtypes = [vp]
+    L.gol_digest.argtypes = [vp, pu64, pu64]
+    L.gol_destroy.argtypes = [vp]
+    L.gol_destroy.restype = None
+    L.gol_last_error.argtypes = []
+    L.gol_last_error.restype = ctypes.c_char_p
+    L.gol_set_timing.argtypes = [vp, i32]
+    L.gol_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
+    L.gol_reset_timing.argtypes = [vp]
+    L.gol_info.argtypes = [vp, pu64, pu64, pu64, pu64, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    L.gol_rank_rows.argtypes = [u64, i32, i32, pu64, pu64]
+    L.gol_comm_unique_id.argtypes = [ctypes.c_char_p]
+    for name in ["gol_create", "gol_create_rank", "gol_load_ascii", "gol_store_ascii",
+                 "gol_load_packed", "gol_store_packed", "gol_init_random", "gol_step",
+                 "gol_sync", "gol_digest", "gol_set_timing", "gol_get_timing",
+                 "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id"]:
+        getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def _check(st):
+    if st != GOL_OK:
+        raise GolError(st, lib().gol_last_error().decode(errors="replace"))
+
+
+def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_depth=0,
+                halo_depth=0, rows_per_wave=0):
+    c = Config()
+    lib().gol_config_init(ctypes.byref(c))
+    c.birth_mask, c.survive_mask = rule
+    c.device = device
+    c.semantics = semantics
+    c.ref_ranks = ref_ranks
+    c.tb_depth = tb_depth
+    c.halo_depth = halo_depth
+    c.rows_per_wave = rows_per_wave
+    return c
+
+
+def rank_rows(h, nranks, rank):
+    r0, n = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().gol_rank_rows(h, nranks, rank, ctypes.byref(r0), ctypes.byref(n)))
+    return r0.value, n.value
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().gol_comm_unique_id(buf))
+    return buf.raw
+
+
+class Engine:
+    """One field (or one rank's stripe of it) resident on one GPU."""
+
+    def __init__(self, h, w, rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1,
+                 tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None):
+        self.h, self.w = h, w
+        self.wq = (w + 63) // 64
+        cfg = make_config(rule, device, semantics, ref_ranks, tb_depth, halo_depth,
+                          rows_per_wave)
+        handle = ctypes.c_void_p()
+        if rank is None:
+            _check(lib().gol_create(h, w, ctypes.byref(cfg), ctypes.byref(handle)))
+        else:
+            if uid is None or len(uid) != 128:
+                raise GolError(GOL_EINVAL, "rank engines need a 128-byte RCCL unique id")
+            _check(lib().gol_create_rank(h, w, ctypes.byref(cfg), rank, nranks, uid,
+                                         ctypes.byref(handle)))
+        self._h = handle
+        h_, w_, r0, rows = (ctypes.c_uint64() for _ in range(4))
+        k, hx = ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().gol_info(self._h, ctypes.byref(h_), ctypes.byref(w_), ctypes.byref(r0),
+                              ctypes.byref(rows), ctypes.byref(k), ctypes.byref(hx)))
+        self.row0, self.rows, self.tb_depth, self.halo_depth = r0.value, rows.value, k.value, hx.value
+
+    def close(self):
+        if self._h:
+            lib().gol_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def load_ascii(self, data: bytes):
+        _check(lib().gol_load_ascii(self._h, data, len(data)))
+
+    def store_ascii(self, nbytes=None) -> bytes:
+        n = nbytes if nbytes is not None else self.rows * (self.w + 1)
+        buf = ctypes.create_string_buffer(n)
+        _check(lib().gol_store_ascii(self._h, buf, n))
+        return buf.raw
+
+    def load_packed(self, arr):
+        import numpy as np
+        a = np.ascontiguousarray(arr, dtype=np.uint64)
+        _check(lib().gol_load_packed(self._h, a.ctypes.data, a.shape[1]))
+
+    def store_packed(self, rows=None):
+        import numpy as np
+        rows = rows if rows is not None else self.rows
+        a = np.zeros((rows, self.wq), dtype=np.uint64)
+        _check(lib().gol_store_packed(self._h, a.ctypes.data, self.wq))
+        return a
+
+    def init_random(self, seed=1):
+        _check(lib().gol_init_random(self._h, seed))
+
+    def step(self, gens):
+        _check(lib().gol_step(self._h, gens))
+
+    def sync(self):
+        _check(lib().gol_sync(self._h))
+
+    def digest(self):
+        live, hsh = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().gol_digest(self._h, ctypes.byref(live), ctypes.byref(hsh)))
+        return live.value, hsh.value
+
+    def set_timing(self, on=True):
+        _check(lib().gol_set_timing(self._h, 1 if on else 0))
+
+    def reset_timing(self):
+        _check(lib().gol_reset_timing(self._h))
+
+    def timing(self):
+        t = Timing()
+        _check(lib().gol_get_timing(self._h, ctypes.byref(t)))
+        return {"launches": t.launches, "kernel_ms": t.kernel_ms, "cell_gens": t.cell_gens,
+                "cell_gens_computed": t.cell_gens_computed}

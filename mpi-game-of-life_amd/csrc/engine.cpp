@@ -1,0 +1,749 @@
+// engine.cpp -- host side of libgol.so: the C ABI of include/gol.h.
+//
+// Owns device memory, the HIP stream, the RCCL communicator and the launch
+// plans.  Mirrors main()'s flow in Parallel_Life_MPI.cpp:190-240: create
+// (readGridFromFile's allocation :88-89) -> load (:91-99) -> step (the epoch loop
+// :215-221 with the halo exchange :104-145) -> store (:157-164).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/gol.h"
+#include "life_internal.h"
+
+using gol::SegDesc;
+using gol::StepArgs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+gol_status fail(gol_status st, const std::string& msg)
+{
+    g_last_error = msg;
+    return st;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return fail(_e == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP,                  \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                 \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                      \
+    do {                                                                                    \
+        ncclResult_t _r = (expr);                                                           \
+        if (_r != ncclSuccess)                                                              \
+            return fail(GOL_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(_r));     \
+    } while (0)
+
+constexpr uint32_t kDepths[] = {16, 8, 4, 2, 1};
+
+uint64_t last_mask(uint64_t w)
+{
+    const unsigned rem = (unsigned)(w & 63);
+    return rem ? ((1ull << rem) - 1ull) : ~0ull;
+}
+
+// Parallel_Life_MPI.cpp:70-81 -- rank r's extended stripe [start, start+rows).
+bool ref_stripe(uint64_t h, uint64_t P, uint64_t r, uint64_t* start, uint64_t* rows)
+{
+    if (P == 0 || r >= P || h / P == 0) return false;
+    uint64_t chunk = h / P, s = r * chunk;
+    if (r != 0) {
+        s--;
+        chunk++;
+    }
+    chunk += (r == P - 1) ? h % P : 1;
+    *start = s;
+    *rows = chunk;
+    return true;
+}
+
+// Pack `rows` ASCII lines (w cells + '\n') into `stride`-word rows; threaded.
+bool pack_ascii(const char* buf, uint64_t rows, uint64_t w, uint64_t stride, uint64_t* dst)
+{
+    const uint64_t wq = (w + 63) / 64;
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (rows * w < (1u << 20)) nt = 1;
+    std::vector<std::thread> th;
+    std::vector<char> bad(nt, 0);
+    for (unsigned t = 0; t < nt; ++t) {
+        th.emplace_back([=, &bad]() {
+            const uint64_t r0 = rows * t / nt, r1 = rows * (t + 1) / nt;
+            for (uint64_t r = r0; r < r1; ++r) {
+                const char* line = buf + r * (w + 1);
+                if (line[w] != '\n') bad[t] = 1;
+                uint64_t* out = dst + r * stride;
+                for (uint64_t q = 0; q < stride; ++q) {
+                    uint64_t v = 0;
+                    if (q < wq) {
+                        const uint64_t c0 = q * 64, n = std::min<uint64_t>(64, w - c0);
+                        for (uint64_t j = 0; j < n; ++j)
+                            v |= (uint64_t)(line[c0 + j] == '1') << j;
+                    }
+                    out[q] = v;
+                }
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    for (char b : bad)
+        if (b) return false;
+    return true;
+}
+
+void unpack_ascii(const uint64_t* src, uint64_t rows, uint64_t w, uint64_t stride, char* buf)
+{
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (rows * w < (1u << 20)) nt = 1;
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) {
+        th.emplace_back([=]() {
+            const uint64_t r0 = rows * t / nt, r1 = rows * (t + 1) / nt;
+            for (uint64_t r = r0; r < r1; ++r) {
+                char* line = buf + r * (w + 1);
+                const uint64_t* in = src + r * stride;
+                for (uint64_t c = 0; c < w; ++c) line[c] = ((in[c >> 6] >> (c & 63)) & 1) ? '1' : '0';
+                line[w] = '\n';
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+}
+
+// A host-visible region of the field: buffer rows [buf_row, buf_row+rows) are field
+// rows [glob_row, glob_row+rows); it corresponds to the caller's ASCII/packed rows
+// [user_row, user_row+rows).
+struct Region {
+    uint64_t buf_row, glob_row, user_row, rows;
+};
+
+}  // namespace
+
+struct gol_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint64_t H = 0, W = 0, wq = 0, stride = 0, lastmask = 0;
+    uint32_t birth = 0, survive = 0;
+    gol::RuleKind rule = gol::RULE_REF;
+    uint32_t K = 8;
+    uint32_t rows_per_wave = 0;
+    uint32_t sem = GOL_SEM_GLOBAL;
+    uint32_t P = 1;
+
+    // rank geometry (single-GPU: rank 0 of 1, Hx = 0)
+    int rank = 0, nranks = 1;
+    uint64_t row0 = 0, R = 0, Hx = 0;
+    ncclComm_t comm = nullptr;
+
+    uint64_t buf_rows = 0;
+    uint64_t* alloc[2] = {nullptr, nullptr};
+    uint64_t* buf[2] = {nullptr, nullptr};
+    int cur = 0;
+
+    // plans: plan p = a device table of nseg SegDesc (+ host copy)
+    struct Plan {
+        std::vector<SegDesc> segs;
+        int64_t total_units = 0;
+        SegDesc* dev = nullptr;
+    };
+    std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: plans[c-1] for shrink c
+    int32_t strips = 0;
+
+    std::vector<Region> user_regions;  // load/store mapping (own output rows)
+    std::vector<Region> load_regions;  // rows loaded (REF_STRIPES loads overlaps too)
+
+    unsigned long long* d_acc = nullptr;
+
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_free;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    std::vector<double> pending_cells, pending_cells_comp;
+    gol_timing tm{};
+};
+
+namespace {
+
+int64_t plan_units(const std::vector<SegDesc>& segs, int32_t strips)
+{
+    int64_t u = 0;
+    for (const auto& s : segs) u += s.nblk * strips;
+    return u;
+}
+
+void finish_segs(std::vector<SegDesc>& segs, int64_t rpw, int32_t strips)
+{
+    int64_t unit = 0;
+    for (auto& s : segs) {
+        const int64_t n = std::max<int64_t>(0, s.out_hi - s.out_lo);
+        s.nblk = (n + rpw - 1) / rpw;
+        s.unit0 = unit;
+        unit += s.nblk * strips;
+    }
+}
+
+gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
+{
+    // choose rows per wavefront: enough wavefronts to fill 256 CUs several times
+    int64_t rpw = e->rows_per_wave;
+    if (rpw == 0) {
+        rpw = 512;
+        const int64_t min_rpw = std::max<int64_t>(16, 2 * e->K);
+        while (rpw > min_rpw) {
+            std::vector<SegDesc> t = raw[0];
+            finish_segs(t, rpw, e->strips);
+            if (plan_units(t, e->strips) >= 4096) break;
+            rpw /= 2;
+        }
+    }
+    e->rows_per_wave = (uint32_t)rpw;
+    for (const auto& r : raw) {
+        gol_engine::Plan p;
+        p.segs = r;
+        finish_segs(p.segs, rpw, e->strips);
+        p.total_units = plan_units(p.segs, e->strips);
+        HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * p.segs.size()));
+        HIP_TRY(hipMemcpy(p.dev, p.segs.data(), sizeof(SegDesc) * p.segs.size(),
+                          hipMemcpyHostToDevice));
+        e->plans.push_back(p);
+    }
+    return GOL_OK;
+}
+
+gol_status check_cfg(const gol_config* cfg)
+{
+    if (!cfg) return fail(GOL_EINVAL, "null config");
+    if (cfg->birth_mask >= 512 || cfg->survive_mask >= 512)
+        return fail(GOL_EINVAL, "rule masks must be 9-bit");
+    if (cfg->tb_depth != 0 && cfg->tb_depth != 1 && cfg->tb_depth != 2 && cfg->tb_depth != 4 &&
+        cfg->tb_depth != 8 && cfg->tb_depth != 16)
+        return fail(GOL_EINVAL, "tb_depth must be 0 (auto), 1, 2, 4, 8 or 16");
+    if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
+    return GOL_OK;
+}
+
+// Common construction; geometry (row0, R, Hx, rank) already set.
+gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* cfg)
+{
+    e->H = h;
+    e->W = w;
+    e->wq = (w + 63) / 64;
+    e->stride = (e->wq + 7) / 8 * 8;
+    e->lastmask = last_mask(w);
+    e->birth = cfg->birth_mask;
+    e->survive = cfg->survive_mask;
+    if (e->birth == GOL_REF_BIRTH && e->survive == GOL_REF_SURVIVE)
+        e->rule = gol::RULE_REF;
+    else if (e->birth == GOL_CONWAY_BIRTH && e->survive == GOL_CONWAY_SURVIVE)
+        e->rule = gol::RULE_CONWAY;
+    else
+        e->rule = gol::RULE_GENERIC;
+    e->K = cfg->tb_depth ? cfg->tb_depth : 8;
+    e->rows_per_wave = cfg->rows_per_wave;
+    e->sem = cfg->semantics;
+    e->strips = (int32_t)((e->wq + gol::kStripOut - 1) / gol::kStripOut);
+
+    if (cfg->device >= 0) HIP_TRY(hipSetDevice(cfg->device));
+    HIP_TRY(hipGetDevice(&e->device));
+    HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+
+    std::vector<std::vector<SegDesc>> raw;
+    if (e->nranks > 1) {
+        // local row i <-> field row row0 - Hx + i; buffer holds R + 2Hx rows
+        e->buf_rows = e->R + 2 * e->Hx;
+        const int64_t glob0 = (int64_t)e->row0 - (int64_t)e->Hx;
+        const int64_t in_field_lo = std::max<int64_t>(0, -glob0);
+        const int64_t in_field_hi =
+            std::min<int64_t>((int64_t)e->buf_rows, (int64_t)h - glob0);
+        for (uint64_t c = 1; c <= e->Hx; ++c) {
+            SegDesc s{};
+            s.base_row = 0;
+            s.in_rows = (int64_t)e->buf_rows;
+            s.glob0 = glob0;
+            s.field_h = (int64_t)h;
+            s.out_lo = std::max<int64_t>((int64_t)c, in_field_lo);
+            s.out_hi = std::min<int64_t>((int64_t)(e->buf_rows - c), in_field_hi);
+            raw.push_back({s});
+        }
+        e->user_regions.push_back({e->Hx, e->row0, 0, e->R});
+        e->load_regions = e->user_regions;
+    } else if (e->sem == GOL_SEM_REF_STRIPES) {
+        e->P = cfg->ref_ranks ? cfg->ref_ranks : 1;
+        if (h / e->P == 0) return fail(GOL_EINVAL, "REF_STRIPES needs h >= ref_ranks");
+        std::vector<SegDesc> segs;
+        uint64_t base = 0;
+        const uint64_t c = h / e->P;
+        for (uint32_t r = 0; r < e->P; ++r) {
+            uint64_t s0, n;
+            ref_stripe(h, e->P, r, &s0, &n);
+            SegDesc s{};
+            s.base_row = (int64_t)base;
+            s.in_rows = (int64_t)n;
+            s.glob0 = 0;
+            s.field_h = (int64_t)n;
+            s.out_lo = 0;
+            s.out_hi = (int64_t)n;
+            segs.push_back(s);
+            e->load_regions.push_back({base, s0, s0, n});
+            // writeDataToFile (:149-175): own rows [r*c, (r+1)*c), last rank to h
+            const uint64_t lo = r * c, hi = (r == e->P - 1) ? h : (r + 1) * c;
+            e->user_regions.push_back({base + (lo - s0), lo, lo, hi - lo});
+            base += n;
+        }
+        e->buf_rows = base;
+        raw.push_back(segs);
+    } else {
+        e->buf_rows = h;
+        SegDesc s{};
+        s.base_row = 0;
+        s.in_rows = (int64_t)h;
+        s.glob0 = 0;
+        s.field_h = (int64_t)h;
+        s.out_lo = 0;
+        s.out_hi = (int64_t)h;
+        raw.push_back({s});
+        e->user_regions.push_back({0, 0, 0, h});
+        e->load_regions = e->user_regions;
+    }
+
+    const size_t words = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
+    for (int b = 0; b < 2; ++b) {
+        HIP_TRY(hipMalloc(&e->alloc[b], words * sizeof(uint64_t)));
+        HIP_TRY(hipMemsetAsync(e->alloc[b], 0, words * sizeof(uint64_t), e->stream));
+        e->buf[b] = e->alloc[b] + (size_t)gol::kGuardRows * e->stride;
+    }
+    HIP_TRY(hipMalloc(&e->d_acc, 2 * sizeof(unsigned long long)));
+    gol_status st = build_plans(e, raw);
+    if (st != GOL_OK) return st;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return GOL_OK;
+}
+
+gol_status flush_timing(gol_engine* e)
+{
+    for (size_t i = 0; i < e->ev_pending.size(); ++i) {
+        auto& p = e->ev_pending[i];
+        HIP_TRY(hipEventSynchronize(p.second));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.first, p.second));
+        e->tm.launches += 1;
+        e->tm.kernel_ms += ms;
+        e->tm.cell_gens += e->pending_cells[i];
+        e->tm.cell_gens_computed += e->pending_cells_comp[i];
+        e->ev_free.push_back(p.first);
+        e->ev_free.push_back(p.second);
+    }
+    e->ev_pending.clear();
+    e->pending_cells.clear();
+    e->pending_cells_comp.clear();
+    return GOL_OK;
+}
+
+gol_status get_event(gol_engine* e, hipEvent_t* ev)
+{
+    if (e->ev_free.empty()) {
+        HIP_TRY(hipEventCreate(ev));
+        return GOL_OK;
+    }
+    *ev = e->ev_free.back();
+    e->ev_free.pop_back();
+    return GOL_OK;
+}
+
+gol_status launch(gol_engine* e, int plan, uint32_t depth)
+{
+    const auto& p = e->plans[plan];
+    StepArgs a{};
+    a.in = e->buf[e->cur];
+    a.out = e->buf[e->cur ^ 1];
+    a.segs = p.dev;
+    a.nseg = (int32_t)p.segs.size();
+    a.strips = e->strips;
+    a.stride = (int64_t)e->stride;
+    a.wq = (int64_t)e->wq;
+    a.lastmask = e->lastmask;
+    a.rows_per_wave = e->rows_per_wave;
+    a.total_units = p.total_units;
+    a.birth = e->birth;
+    a.survive = e->survive;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e->timing) {
+        gol_status st = get_event(e, &e0);
+        if (st == GOL_OK) st = get_event(e, &e1);
+        if (st != GOL_OK) return st;
+        HIP_TRY(hipEventRecord(e0, e->stream));
+    }
+    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->stream));
+    if (e->timing) {
+        HIP_TRY(hipEventRecord(e1, e->stream));
+        e->ev_pending.push_back({e0, e1});
+        double own = 0, comp = 0;
+        for (const auto& r : e->user_regions) own += (double)r.rows;
+        for (const auto& s : p.segs) comp += (double)(s.out_hi - s.out_lo);
+        e->pending_cells.push_back(own * (double)e->W * depth);
+        e->pending_cells_comp.push_back(comp * (double)e->W * depth);
+    }
+    e->cur ^= 1;
+    return GOL_OK;
+}
+
+uint32_t pick_depth(uint32_t K, uint64_t remaining)
+{
+    for (uint32_t d : kDepths)
+        if (d <= K && d <= remaining) return d;
+    return 1;
+}
+
+// Halo exchange (replaces exchangeGridData, Parallel_Life_MPI.cpp:104-145, whose
+// receives land in copies): Hx rows each way with the up/down neighbour.
+gol_status exchange(gol_engine* e)
+{
+    uint64_t* b = e->buf[e->cur];
+    const size_t n = (size_t)e->Hx * e->stride;
+    const size_t S = e->stride;
+    NCCL_TRY(ncclGroupStart());
+    if (e->rank > 0) {
+        NCCL_TRY(ncclSend(b + e->Hx * S, n, ncclUint64, e->rank - 1, e->comm, e->stream));
+        NCCL_TRY(ncclRecv(b, n, ncclUint64, e->rank - 1, e->comm, e->stream));
+    }
+    if (e->rank < e->nranks - 1) {
+        NCCL_TRY(ncclSend(b + e->R * S, n, ncclUint64, e->rank + 1, e->comm, e->stream));
+        NCCL_TRY(ncclRecv(b + (e->R + e->Hx) * S, n, ncclUint64, e->rank + 1, e->comm,
+                          e->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return GOL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void gol_config_init(gol_config* cfg)
+{
+    if (!cfg) return;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->birth_mask = GOL_REF_BIRTH;
+    cfg->survive_mask = GOL_REF_SURVIVE;
+    cfg->device = -1;
+    cfg->semantics = GOL_SEM_GLOBAL;
+    cfg->ref_ranks = 1;
+}
+
+const char* gol_last_error(void) { return g_last_error.c_str(); }
+
+gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine** out)
+{
+    if (!out) return fail(GOL_EINVAL, "null out");
+    *out = nullptr;
+    gol_status st = check_cfg(cfg);
+    if (st != GOL_OK) return st;
+    if (h == 0 || w == 0) return fail(GOL_EINVAL, "h and w must be >= 1");
+    if (h > (1ull << 40) || w > (1ull << 40)) return fail(GOL_EINVAL, "field too large");
+    gol_engine* e = new (std::nothrow) gol_engine();
+    if (!e) return fail(GOL_ENOMEM, "host allocation");
+    e->R = h;
+    st = init_common(e, h, w, cfg);
+    if (st != GOL_OK) {
+        std::string msg = g_last_error;
+        gol_destroy(e);
+        g_last_error = msg;
+        return st;
+    }
+    *out = e;
+    return GOL_OK;
+}
+
+gol_status gol_rank_rows(uint64_t h, int nranks, int rank, uint64_t* row0, uint64_t* rows)
+{
+    if (nranks <= 0 || rank < 0 || rank >= nranks || !row0 || !rows)
+        return fail(GOL_EINVAL, "bad rank/nranks");
+    const uint64_t base = h / (uint64_t)nranks, extra = h % (uint64_t)nranks;
+    const uint64_t r = (uint64_t)rank;
+    *rows = base + (r < extra ? 1 : 0);
+    *row0 = r * base + std::min(r, extra);
+    return GOL_OK;
+}
+
+gol_status gol_comm_unique_id(uint8_t id[128])
+{
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    NCCL_TRY(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, 128);
+    return GOL_OK;
+}
+
+gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
+                           const uint8_t id[128], gol_engine** out)
+{
+    if (!out || !id) return fail(GOL_EINVAL, "null argument");
+    *out = nullptr;
+    gol_status st = check_cfg(cfg);
+    if (st != GOL_OK) return st;
+    if (cfg->semantics != GOL_SEM_GLOBAL)
+        return fail(GOL_EINVAL, "rank engines implement GLOBAL semantics only");
+    if (h == 0 || w == 0) return fail(GOL_EINVAL, "h and w must be >= 1");
+    uint64_t row0, rows;
+    st = gol_rank_rows(h, nranks, rank, &row0, &rows);
+    if (st != GOL_OK) return st;
+    gol_engine* e = new (std::nothrow) gol_engine();
+    if (!e) return fail(GOL_ENOMEM, "host allocation");
+    e->rank = rank;
+    e->nranks = nranks;
+    e->row0 = row0;
+    e->R = rows;
+    const uint32_t K = cfg->tb_depth ? cfg->tb_depth : 8;
+    uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 4 * (uint64_t)K;
+    // a rank sends its first/last Hx own rows: every rank needs R >= Hx
+    const uint64_t minR = h / (uint64_t)nranks;
+    if (Hx > minR) Hx = minR;
+    if (Hx == 0) {
+        delete e;
+        return fail(GOL_EINVAL, "fewer rows than ranks");
+    }
+    e->Hx = nranks > 1 ? Hx : 0;
+    if (nranks > 1) {
+        st = init_common(e, h, w, cfg);
+        if (st == GOL_OK) {
+            ncclUniqueId u;
+            std::memcpy(&u, id, 128);
+            ncclResult_t r = ncclCommInitRank(&e->comm, nranks, u, rank);
+            if (r != ncclSuccess)
+                st = fail(GOL_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+    } else {
+        gol_config c1 = *cfg;
+        st = init_common(e, h, w, &c1);
+    }
+    if (st != GOL_OK) {
+        std::string msg = g_last_error;
+        gol_destroy(e);
+        g_last_error = msg;
+        return st;
+    }
+    *out = e;
+    return GOL_OK;
+}
+
+void gol_destroy(gol_engine* e)
+{
+    if (!e) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->comm) (void)ncclCommDestroy(e->comm);
+    for (auto& p : e->plans)
+        if (p.dev) (void)hipFree(p.dev);
+    for (int b = 0; b < 2; ++b)
+        if (e->alloc[b]) (void)hipFree(e->alloc[b]);
+    if (e->d_acc) (void)hipFree(e->d_acc);
+    for (auto& p : e->ev_pending) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    for (auto ev : e->ev_free) (void)hipEventDestroy(ev);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+static uint64_t user_rows(const gol_engine* e)
+{
+    uint64_t n = 0;
+    for (const auto& r : e->user_regions) n += r.rows;
+    return n;
+}
+
+static uint64_t load_rows_needed(const gol_engine* e)
+{
+    // rows of the caller's buffer that a load reads: the whole field for
+    // GLOBAL/REF_STRIPES, own rows for a rank engine
+    return e->nranks > 1 ? e->R : e->H;
+}
+
+gol_status gol_load_packed(gol_engine* e, const uint64_t* words, uint64_t rs)
+{
+    if (!e || !words) return fail(GOL_EINVAL, "null argument");
+    if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
+    HIP_TRY(hipSetDevice(e->device));
+    // clear everything (halos, unused rows) then copy each region, masking pad bits
+    const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
+    HIP_TRY(hipMemsetAsync(e->alloc[e->cur], 0, words_all * 8, e->stream));
+    std::vector<uint64_t> tmp;
+    for (const auto& r : e->load_regions) {
+        tmp.assign((size_t)r.rows * e->stride, 0);
+        const uint64_t urow = e->nranks > 1 ? 0 : r.user_row;
+        for (uint64_t i = 0; i < r.rows; ++i) {
+            const uint64_t* src = words + (urow + i) * rs;
+            uint64_t* dst = tmp.data() + i * e->stride;
+            for (uint64_t q = 0; q < e->wq; ++q) dst[q] = src[q];
+            dst[e->wq - 1] &= e->lastmask;
+        }
+        HIP_TRY(hipMemcpyAsync(e->buf[e->cur] + r.buf_row * e->stride, tmp.data(),
+                               tmp.size() * 8, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    }
+    return GOL_OK;
+}
+
+gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
+{
+    if (!e || !buf) return fail(GOL_EINVAL, "null argument");
+    const uint64_t rows = load_rows_needed(e);
+    if (len != rows * (e->W + 1))
+        return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
+                                    std::to_string(rows * (e->W + 1)) + ", got " +
+                                    std::to_string(len));
+    std::vector<uint64_t> packed((size_t)rows * e->stride);
+    if (!pack_ascii(buf, rows, e->W, e->stride, packed.data()))
+        return fail(GOL_EINVAL, "malformed ASCII: a line is not w cells followed by '\\n'");
+    return gol_load_packed(e, packed.data(), e->stride);
+}
+
+gol_status gol_store_packed(gol_engine* e, uint64_t* words, uint64_t rs)
+{
+    if (!e || !words) return fail(GOL_EINVAL, "null argument");
+    if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
+    HIP_TRY(hipSetDevice(e->device));
+    std::vector<uint64_t> tmp;
+    for (const auto& r : e->user_regions) {
+        tmp.resize((size_t)r.rows * e->stride);
+        HIP_TRY(hipMemcpyAsync(tmp.data(), e->buf[e->cur] + r.buf_row * e->stride,
+                               tmp.size() * 8, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        const uint64_t urow = e->nranks > 1 ? 0 : r.user_row;
+        for (uint64_t i = 0; i < r.rows; ++i)
+            std::memcpy(words + (urow + i) * rs, tmp.data() + i * e->stride, e->wq * 8);
+    }
+    return GOL_OK;
+}
+
+gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
+{
+    if (!e || !buf) return fail(GOL_EINVAL, "null argument");
+    const uint64_t rows = user_rows(e);
+    if (len != rows * (e->W + 1))
+        return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
+                                    std::to_string(rows * (e->W + 1)));
+    std::vector<uint64_t> packed((size_t)rows * e->stride);
+    gol_status st = gol_store_packed(e, packed.data(), e->stride);
+    if (st != GOL_OK) return st;
+    unpack_ascii(packed.data(), rows, e->W, e->stride, buf);
+    return GOL_OK;
+}
+
+gol_status gol_init_random(gol_engine* e, uint64_t seed)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
+    HIP_TRY(hipMemsetAsync(e->alloc[e->cur], 0, words_all * 8, e->stream));
+    for (const auto& r : e->load_regions)
+        HIP_TRY(gol::launch_init_random(e->buf[e->cur], (int64_t)e->stride, (int64_t)e->wq,
+                                        e->lastmask, (int64_t)r.buf_row, (int64_t)r.glob_row,
+                                        (int64_t)r.rows, seed, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return GOL_OK;
+}
+
+gol_status gol_step(gol_engine* e, uint64_t generations)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    uint64_t left = generations;
+    if (e->nranks > 1) {
+        while (left > 0) {
+            const uint64_t round = std::min<uint64_t>(left, e->Hx);
+            gol_status st = exchange(e);
+            if (st != GOL_OK) return st;
+            uint64_t done = 0;
+            while (done < round) {
+                const uint32_t d = pick_depth(e->K, round - done);
+                done += d;
+                st = launch(e, (int)(done - 1), d);
+                if (st != GOL_OK) return st;
+            }
+            left -= round;
+        }
+        return GOL_OK;
+    }
+    while (left > 0) {
+        const uint32_t d = pick_depth(e->K, left);
+        gol_status st = launch(e, 0, d);
+        if (st != GOL_OK) return st;
+        left -= d;
+    }
+    return GOL_OK;
+}
+
+gol_status gol_sync(gol_engine* e)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return GOL_OK;
+}
+
+gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
+{
+    if (!e || !live || !hash) return fail(GOL_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemsetAsync(e->d_acc, 0, 2 * sizeof(unsigned long long), e->stream));
+    for (const auto& r : e->user_regions)
+        HIP_TRY(gol::launch_digest(e->buf[e->cur], (int64_t)e->stride, (int64_t)e->wq,
+                                   (int64_t)r.buf_row, (int64_t)r.glob_row, (int64_t)r.rows,
+                                   e->d_acc, e->stream));
+    unsigned long long acc[2];
+    HIP_TRY(hipMemcpyAsync(acc, e->d_acc, sizeof(acc), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    *live = acc[0];
+    *hash = acc[1];
+    return GOL_OK;
+}
+
+gol_status gol_set_timing(gol_engine* e, int enable)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    e->timing = enable != 0;
+    return GOL_OK;
+}
+
+gol_status gol_get_timing(gol_engine* e, gol_timing* out)
+{
+    if (!e || !out) return fail(GOL_EINVAL, "null argument");
+    gol_status st = flush_timing(e);
+    if (st != GOL_OK) return st;
+    *out = e->tm;
+    return GOL_OK;
+}
+
+gol_status gol_reset_timing(gol_engine* e)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    gol_status st = flush_timing(e);
+    if (st != GOL_OK) return st;
+    e->tm = gol_timing{};
+    return GOL_OK;
+}
+
+gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uint64_t* rows,
+                    uint32_t* tb_depth, uint32_t* halo_depth)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (h) *h = e->H;
+    if (w) *w = e->W;
+    if (row0) *row0 = e->row0;
+    if (rows) *rows = e->nranks > 1 ? e->R : e->H;
+    if (tb_depth) *tb_depth = e->K;
+    if (halo_depth) *halo_depth = (uint32_t)e->Hx;
+    return GOL_OK;
+}
+
+}  // extern "C"

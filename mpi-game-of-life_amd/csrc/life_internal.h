@@ -1,0 +1,70 @@
+// Internal interface between the host engine (engine.cpp) and the HIP kernels
+// (life_kernels.hip).  Not part of the public C ABI (include/gol.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gol {
+
+// Rule specialisations of the stencil kernel.
+enum RuleKind : int {
+    RULE_REF = 0,     // birth = {}, survive = {2}: the reference's effective rule
+    RULE_CONWAY = 1,  // birth = {3}, survive = {2,3}
+    RULE_GENERIC = 2  // any 9-bit mask pair, full 0..8 neighbour count
+};
+
+// One independent field region streamed by the stencil kernel.
+//   Buffer row (base_row + i) holds segment-local row i.  Local row i is field row
+//   (glob0 + i); field rows outside [0, field_h) are dead (never loaded, forced 0).
+//   The kernel reads local rows [out_lo - K, out_hi + K) (only those inside
+//   [0, in_rows) and inside the field; others read as dead) and writes local rows
+//   [out_lo, out_hi) of the output buffer.
+struct SegDesc {
+    int64_t base_row;
+    int64_t in_rows;
+    int64_t glob0;
+    int64_t field_h;
+    int64_t out_lo, out_hi;
+    int64_t nblk;   // row blocks of rows_per_wave rows
+    int64_t unit0;  // index of this segment's first wavefront in the launch
+};
+
+// Output words per wavefront strip: 64 lanes each hold one 64-bit word; lanes 0
+// and 63 are the horizontal halo (valid up to 63 fused generations).
+constexpr int kStripOut = 62;
+constexpr int kWavesPerBlock = 4;
+// Zeroed guard rows allocated before/after every state buffer so that the
+// streaming loads (K rows of halo + prefetch distance) never leave the allocation.
+constexpr int kGuardRows = 64;
+constexpr int kMaxDepth = 16;
+
+struct StepArgs {
+    const uint64_t* in;   // state buffer row 0 (guard rows precede it)
+    uint64_t* out;
+    const SegDesc* segs;  // device table
+    int32_t nseg;
+    int32_t strips;       // ceil(wq / kStripOut)
+    int64_t stride;       // words per buffer row
+    int64_t wq;           // words per field row = ceil(w / 64)
+    uint64_t lastmask;    // valid bits of word wq-1
+    int64_t rows_per_wave;
+    int64_t total_units;  // wavefronts in the launch
+    uint32_t birth, survive;
+};
+
+// Launch `depth` fused generations (depth in {1,2,4,8,16}).
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, hipStream_t s);
+
+// Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field
+// rows [glob_row0, glob_row0+nrows).
+hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_t lastmask,
+                              int64_t row_base, int64_t glob_row0, int64_t nrows,
+                              uint64_t seed, hipStream_t s);
+
+// Adds popcount and hash of buffer rows [row_base, row_base+nrows) (field rows
+// glob_row0..) into acc[0], acc[1].
+hipError_t launch_digest(const uint64_t* buf, int64_t stride, int64_t wq, int64_t row_base,
+                         int64_t glob_row0, int64_t nrows, unsigned long long* acc,
+                         hipStream_t s);
+
+}  // namespace gol

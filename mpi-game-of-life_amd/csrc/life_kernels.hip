@@ -1,0 +1,322 @@
+// life_kernels.hip -- gfx950 kernels of the Game of Life engine.
+//
+// Hot path: the per-generation update of Parallel_Life_MPI.cpp (countNeighbours
+// :16-35 + updateGrid :37-54), restated on a bit-packed field (64 cells per
+// uint64, bit j of word q = column 64q+j) and fused over K generations per
+// launch (temporal blocking).
+//
+// Kernel shape (one wavefront = one work unit, no LDS, no barriers):
+//   * A wavefront owns a strip of 64 consecutive words of a row (lane l holds
+//     word strip*62 - 1 + l); lanes 0 and 63 are the horizontal halo, so each
+//     strip outputs 62 words.  Horizontal neighbour bits come from the adjacent
+//     lanes by DPP wave shifts (wave_shr:1 / wave_shl:1) and v_alignbit funnel
+//     shifts.  After g fused generations the contamination from the unknown
+//     words beyond the halo lanes has moved g bits into lanes 0/63, so K <= 63
+//     keeps lanes 1..62 exact.
+//   * The wavefront streams down `rows_per_wave` output rows of its strip, K rows
+//     of vertical halo on each side.  Generation g (1..K) is a pipeline stage that
+//     keeps a 3-row window in registers: for each incoming row it forms the
+//     horizontal 3-cell (H3) and 2-cell (H2, centre excluded) bit-sliced sums
+//     once, and emits the previous row as H3(r-1) + H2(r) + H3(r+1) -> rule.
+//     Stage g consumes the row stage g-1 emitted in the same step.  Each input
+//     row is read once from HBM and each output row written once per K
+//     generations: HBM bytes per cell-generation = 0.25 / K (x halo overhead).
+//   * Field rows outside [0, field_h) are dead (Parallel_Life_MPI.cpp:21-22) and
+//     columns >= w are dead (:26-27): masked on load and -- for rules that can
+//     give birth -- re-masked after every generation.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "life_internal.h"
+
+namespace gol {
+
+namespace {
+
+struct u2 {
+    uint32_t lo, hi;
+};
+
+__device__ __forceinline__ uint32_t lane_from_left(uint32_t v)
+{
+    // DPP wave_shr:1 -- lane l receives lane l-1's value; lane 0 receives 0.
+    return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t lane_from_right(uint32_t v)
+{
+    // DPP wave_shl:1 -- lane l receives lane l+1's value; lane 63 receives 0.
+    return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xf, 0xf, true);
+}
+
+// Per-generation pipeline stage state (all bit-sliced, two 32-bit halves):
+//   H3 of row r-2 (sum, carry), H3 of row r-1, H2 of row r-1, cells of row r-1,
+// where r is the incoming row.
+struct Stage {
+    u2 ps, pc;
+    u2 cs, cc;
+    u2 hs, hc;
+    u2 al;
+};
+
+template <int RULE>
+__device__ __forceinline__ uint32_t rule32(uint32_t as, uint32_t ac, uint32_t bs, uint32_t bc,
+                                           uint32_t es, uint32_t ec, uint32_t alive,
+                                           uint32_t birth, uint32_t survive)
+{
+    // n = A + B + E with A = H3(r-2), B = H2(r-1), E = H3(r): each a 2-bit number.
+    const uint32_t s0 = as ^ bs ^ es;                 // bit 0 of n
+    const uint32_t k0 = (as & bs) | (es & (as ^ bs)); // carry into weight 2
+    const uint32_t p = ac ^ bc ^ ec;                  // weight-2 column sum, bit 0
+    const uint32_t mj = (ac & bc) | (ec & (ac ^ bc)); // weight-2 column sum, carry
+    // n = s0 + 2*(p + k0) + 4*mj;  n in {2,3}  <=>  mj == 0 && p + k0 == 1
+    if constexpr (RULE == RULE_REF) {
+        // Parallel_Life_MPI.cpp:47-50: next = alive && n == 2
+        return alive & ~s0 & (p ^ k0) & ~mj;
+    } else if constexpr (RULE == RULE_CONWAY) {
+        return (p ^ k0) & ~mj & (s0 | alive);
+    } else {
+        const uint32_t n1 = p ^ k0;
+        const uint32_t k1 = p & k0;
+        const uint32_t n2 = mj ^ k1;
+        const uint32_t n3 = mj & k1;
+        uint32_t r = 0;
+#pragma unroll
+        for (int n = 0; n <= 8; ++n) {
+            const uint32_t bsel = (birth >> n) & 1u, ssel = (survive >> n) & 1u;
+            if (bsel | ssel) {
+                const uint32_t eq = ((n & 1) ? s0 : ~s0) & ((n & 2) ? n1 : ~n1) &
+                                    ((n & 4) ? n2 : ~n2) & ((n & 8) ? n3 : ~n3);
+                const uint32_t sel = (ssel ? alive : 0u) | (bsel ? ~alive : 0u);
+                r |= eq & sel;
+            }
+        }
+        return r;
+    }
+}
+
+// One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
+template <int RULE>
+__device__ __forceinline__ u2 stage_step(Stage& st, u2 x, uint32_t birth, uint32_t survive)
+{
+    const uint32_t lh = lane_from_left(x.hi);   // hi half of word q-1
+    const uint32_t rl = lane_from_right(x.lo);  // lo half of word q+1
+    // L: neighbour at column c-1 (bit j <- bit j-1); R: column c+1 (bit j <- bit j+1)
+    const uint32_t Llo = __builtin_amdgcn_alignbit(x.lo, lh, 31);
+    const uint32_t Lhi = __builtin_amdgcn_alignbit(x.hi, x.lo, 31);
+    const uint32_t Rlo = __builtin_amdgcn_alignbit(x.hi, x.lo, 1);
+    const uint32_t Rhi = __builtin_amdgcn_alignbit(rl, x.hi, 1);
+    u2 s2, c2, s3, c3;
+    s2.lo = Llo ^ Rlo;
+    s2.hi = Lhi ^ Rhi;
+    c2.lo = Llo & Rlo;
+    c2.hi = Lhi & Rhi;
+    s3.lo = s2.lo ^ x.lo;
+    s3.hi = s2.hi ^ x.hi;
+    c3.lo = c2.lo | (s2.lo & x.lo);
+    c3.hi = c2.hi | (s2.hi & x.hi);
+    u2 y;
+    y.lo = rule32<RULE>(st.ps.lo, st.pc.lo, st.hs.lo, st.hc.lo, s3.lo, c3.lo, st.al.lo, birth,
+                        survive);
+    y.hi = rule32<RULE>(st.ps.hi, st.pc.hi, st.hs.hi, st.hc.hi, s3.hi, c3.hi, st.al.hi, birth,
+                        survive);
+    st.ps = st.cs;
+    st.pc = st.cc;
+    st.cs = s3;
+    st.cc = c3;
+    st.hs = s2;
+    st.hc = c2;
+    st.al = x;
+    return y;
+}
+
+constexpr int kPrefetch = 4;
+
+template <int K, int RULE>
+__global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
+{
+    constexpr bool kBirths = RULE != RULE_REF;
+    const int lane = threadIdx.x & 63;
+    const int64_t unit =
+        (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (unit >= a.total_units) return;
+
+    int sidx = 0;
+    for (int j = 1; j < a.nseg; ++j)
+        if (unit >= a.segs[j].unit0) sidx = j;
+    const SegDesc sg = a.segs[sidx];
+    const int64_t u = unit - sg.unit0;
+    const int strip = (int)(u % a.strips);
+    const int64_t blk = u / a.strips;
+
+    const int64_t q = (int64_t)strip * kStripOut - 1 + lane;
+    const bool qin = (q >= 0) && (q < a.wq);
+    const uint64_t cm = qin ? ((q == a.wq - 1) ? a.lastmask : ~0ull) : 0ull;
+    const uint32_t cmlo = (uint32_t)cm, cmhi = (uint32_t)(cm >> 32);
+    const int64_t qc = qin ? q : 0;
+
+    const int64_t rb = sg.out_lo + blk * a.rows_per_wave;
+    const int64_t re = min(rb + a.rows_per_wave, sg.out_hi);
+    const int64_t T = (re - rb) + 2 * K;  // input rows streamed
+    const int64_t row_first = rb - K;     // local row of step 0
+
+    const uint64_t* inp = a.in + (sg.base_row + row_first) * a.stride + qc;
+    uint64_t* outp = a.out + (sg.base_row + rb) * a.stride + qc;
+    const bool st_lane = qin && lane >= 1 && lane <= kStripOut;
+
+    // field-row validity of local row i (dead border) and buffer-row validity
+    const int64_t lo_ok = max((int64_t)0, -sg.glob0);             // first local row in field
+    const int64_t hi_ok = min(sg.in_rows, sg.field_h - sg.glob0);  // one past last
+
+    Stage st[K];
+#pragma unroll
+    for (int g = 0; g < K; ++g) {
+        st[g].ps = st[g].pc = st[g].cs = st[g].cc = st[g].hs = st[g].hc = st[g].al = u2{0u, 0u};
+    }
+
+    uint64_t ring[kPrefetch];
+#pragma unroll
+    for (int p = 0; p < kPrefetch; ++p) ring[p] = inp[(int64_t)p * a.stride];
+    const uint64_t* pf = inp + (int64_t)kPrefetch * a.stride;
+
+    for (int64_t t0 = 0; t0 < T; t0 += kPrefetch) {
+#pragma unroll
+        for (int p = 0; p < kPrefetch; ++p) {
+            const int64_t t = t0 + p;
+            const int64_t i = row_first + t;  // incoming local row
+            uint64_t xv = ring[p];
+            ring[p] = *pf;
+            pf += a.stride;
+            const bool ok = (i >= lo_ok) && (i < hi_ok);
+            u2 x;
+            x.lo = ok ? ((uint32_t)xv & cmlo) : 0u;
+            x.hi = ok ? ((uint32_t)(xv >> 32) & cmhi) : 0u;
+#pragma unroll
+            for (int g = 0; g < K; ++g) {
+                x = stage_step<RULE>(st[g], x, a.birth, a.survive);
+                if constexpr (kBirths) {
+                    // emitted row i-(g+1): dead outside the field and beyond column w
+                    const int64_t r = i - (g + 1);
+                    const bool rok = (sg.glob0 + r >= 0) && (sg.glob0 + r < sg.field_h);
+                    x.lo = rok ? (x.lo & cmlo) : 0u;
+                    x.hi = rok ? (x.hi & cmhi) : 0u;
+                }
+            }
+            if (t >= 2 * K && t < T && st_lane) {
+                outp[(t - 2 * K) * a.stride] = ((uint64_t)x.hi << 32) | x.lo;
+            }
+        }
+    }
+}
+
+template <int K>
+hipError_t launch_depth(const StepArgs& a, RuleKind rule, hipStream_t s)
+{
+    const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
+    const dim3 block(64 * kWavesPerBlock);
+    switch (rule) {
+    case RULE_REF:
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF>), grid, block, 0, s, a);
+        break;
+    case RULE_CONWAY:
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY>), grid, block, 0, s, a);
+        break;
+    default:
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC>), grid, block, 0, s, a);
+        break;
+    }
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t idx)
+{
+    uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void init_random_kernel(uint64_t* buf, int64_t stride,
+                                                          int64_t wq, uint64_t lastmask,
+                                                          int64_t row_base, int64_t glob_row0,
+                                                          int64_t nrows, uint64_t seed)
+{
+    const int64_t total = nrows * stride;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = k / stride, q = k - i * stride;
+        uint64_t v = 0;
+        if (q < wq) {
+            v = splitmix64_at(seed, (uint64_t)(glob_row0 + i) * (uint64_t)wq + (uint64_t)q);
+            if (q == wq - 1) v &= lastmask;
+        }
+        buf[(row_base + i) * stride + q] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void digest_kernel(const uint64_t* buf, int64_t stride,
+                                                     int64_t wq, int64_t row_base,
+                                                     int64_t glob_row0, int64_t nrows,
+                                                     unsigned long long* acc)
+{
+    const int64_t total = nrows * wq;
+    uint64_t live = 0, hash = 0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = k / wq, q = k - i * wq;
+        const uint64_t v = buf[(row_base + i) * stride + q];
+        live += (uint64_t)__popcll(v);
+        const uint64_t idx = (uint64_t)(glob_row0 + i) * (uint64_t)wq + (uint64_t)q;
+        hash += splitmix64_at(v ^ splitmix64_at(0, idx), 0);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        live += __shfl_xor(live, off);
+        hash += __shfl_xor(hash, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&acc[0], (unsigned long long)live);
+        atomicAdd(&acc[1], (unsigned long long)hash);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, hipStream_t s)
+{
+    if (a.total_units <= 0) return hipSuccess;
+    switch (depth) {
+    case 1: return launch_depth<1>(a, rule, s);
+    case 2: return launch_depth<2>(a, rule, s);
+    case 4: return launch_depth<4>(a, rule, s);
+    case 8: return launch_depth<8>(a, rule, s);
+    case 16: return launch_depth<16>(a, rule, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_t lastmask,
+                              int64_t row_base, int64_t glob_row0, int64_t nrows, uint64_t seed,
+                              hipStream_t s)
+{
+    if (nrows <= 0) return hipSuccess;
+    const int64_t total = nrows * stride;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(init_random_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, stride,
+                       wq, lastmask, row_base, glob_row0, nrows, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_digest(const uint64_t* buf, int64_t stride, int64_t wq, int64_t row_base,
+                         int64_t glob_row0, int64_t nrows, unsigned long long* acc,
+                         hipStream_t s)
+{
+    if (nrows <= 0) return hipSuccess;
+    const int64_t total = nrows * wq;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(digest_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, stride, wq,
+                       row_base, glob_row0, nrows, acc);
+    return hipGetLastError();
+}
+
+}  // namespace gol

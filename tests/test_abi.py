@@ -1,0 +1,86 @@
+"""CPU suite: the C-ABI library loads, exports every symbol include/gol.h
+declares, and its host-only entry points behave (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "gol.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gol_[a-z_]+)\s*\(", src)))
+
+
+def test_header_matches_binding(pkg):
+    assert declared_symbols() == sorted(pkg.EXPORTS)
+
+
+def test_library_exports_every_symbol(pkg):
+    L = pkg.lib()
+    for name in declared_symbols():
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", pkg.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (gol_[a-z_]+)", out))
+    assert set(declared_symbols()) <= exported
+
+
+def test_library_is_gfx950(pkg):
+    blob = open(pkg.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the embedded code object's target
+
+
+def test_config_defaults(pkg):
+    c = pkg.make_config()
+    assert (c.birth_mask, c.survive_mask) == pkg.REF_RULE
+    assert c.semantics == pkg.SEM_GLOBAL and c.device == -1 and c.tb_depth == 0
+
+
+@pytest.mark.parametrize("h,n", [(65536, 8), (65536, 3), (7, 7), (10, 4), (1500, 8)])
+def test_rank_rows_partition(pkg, h, n):
+    rows = [pkg.rank_rows(h, n, r) for r in range(n)]
+    assert rows[0][0] == 0
+    for (r0, c), (r1, _) in zip(rows, rows[1:]):
+        assert r0 + c == r1
+    assert rows[-1][0] + rows[-1][1] == h
+    assert max(c for _, c in rows) - min(c for _, c in rows) <= 1
+
+
+def test_rank_rows_rejects_bad_args(pkg):
+    with pytest.raises(pkg.GolError):
+        pkg.rank_rows(10, 0, 0)
+    with pytest.raises(pkg.GolError):
+        pkg.rank_rows(10, 2, 2)
+
+
+def test_bad_config_rejected_before_touching_gpu(pkg):
+    for kw in ({"rule": (512, 0)}, {"tb_depth": 3}):
+        with pytest.raises(pkg.GolError) as ei:
+            pkg.Engine(10, 10, **kw)
+        assert ei.value.status == pkg.GOL_EINVAL
+    with pytest.raises(pkg.GolError):
+        pkg.Engine(0, 10)
+
+
+def test_c_abi_from_c(pkg, tmp_path):
+    """The header compiles as C and links against libgol.so (a C caller's view)."""
+    src = tmp_path / "t.c"
+    src.write_text(
+        '#include "gol.h"\n#include <stdio.h>\n'
+        "int main(void){gol_config c; gol_config_init(&c); uint64_t r0=0,n=0;\n"
+        "if (gol_rank_rows(100,3,1,&r0,&n)!=GOL_OK) return 1;\n"
+        "printf(\"%llu %llu %u\\n\",(unsigned long long)r0,(unsigned long long)n,c.survive_mask);"
+        "return 0;}\n")
+    exe = tmp_path / "t"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{ROOT}/include", str(src),
+                    "-o", str(exe), f"-L{os.path.dirname(pkg.LIB_PATH)}", "-lgol",
+                    f"-Wl,-rpath,{os.path.dirname(pkg.LIB_PATH)}"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    assert out.split() == ["34", "33", "4"]

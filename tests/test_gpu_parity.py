@@ -1,0 +1,204 @@
+"""GPU parity: libgol.so (HIP kernels on the MI355X) vs the pinned CPU oracle.
+
+Bar: bit-exact (integer/bit work).  Every call goes through the C ABI; there is
+no CPU fallback in the product, so these tests fail if the kernels are wrong or
+libgol.so cannot reach a GPU.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(GOLDEN, "ref_outputs.json")))
+H, W = GOLD["h"], GOLD["w"]
+DEPTHS = [1, 2, 4, 8, 16]
+
+
+def rules(oracle):
+    return {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}
+
+
+# ---------------------------------------------------------------- golden (C1)
+@pytest.mark.parametrize("case", [c for c in GOLD["cases"] if c["gens"] <= 100],
+                         ids=lambda c: f"np{c['np']}-e{c['gens']}")
+def test_reference_outputs(pkg, ref_data, case):
+    sem = pkg.SEM_GLOBAL if case["np"] == 1 else pkg.SEM_REF_STRIPES
+    with pkg.Engine(H, W, device=0, semantics=sem, ref_ranks=case["np"]) as e:
+        e.load_ascii(ref_data)
+        e.step(case["gens"])
+        e.sync()
+        out = e.store_ascii(H * (W + 1))
+    assert out.count(b"1") == case["live"]
+    assert hashlib.sha256(out).hexdigest() == case["sha256"]
+
+
+def test_reference_1000_generations(pkg, ref_data):
+    case = [c for c in GOLD["cases"] if c["gens"] == 1000][0]
+    with pkg.Engine(H, W, device=0) as e:
+        e.load_ascii(ref_data)
+        e.step(1000)
+        out = e.store_ascii(H * (W + 1))
+    assert hashlib.sha256(out).hexdigest() == case["sha256"]
+
+
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_reference_per_generation(pkg, oracle, ref_data, depth):
+    """Gens 1..8 one at a time and in one call, at every fused depth (the B/S2
+    field reaches a fixed point after ~5 gens, so early gens matter)."""
+    g = oracle.bp_pack(ref_data, H, W)
+    with pkg.Engine(H, W, device=0, tb_depth=depth) as e:
+        e.load_ascii(ref_data)
+        for gen in range(1, 9):
+            e.step(1)
+            g = oracle.bp_run(g, W, 1)
+            assert (e.store_packed() == g).all(), f"gen {gen}"
+
+
+# ------------------------------------------------- random fields, all rules
+SHAPES = [(1, 1), (1, 70), (2, 64), (3, 63), (5, 65), (17, 129), (64, 500), (100, 3969),
+          (33, 3968), (40, 7937), (257, 200)]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: f"{s[0]}x{s[1]}")
+@pytest.mark.parametrize("rule", ["ref", "conway", "highlife"])
+def test_random_fields_every_depth(pkg, oracle, shape, rule):
+    h, w = shape
+    R = rules(oracle)[rule]
+    seed = h * 1000 + w
+    want = {}
+    g = oracle.bp_random(h, w, seed)
+    for gens in (1, 3, 16, 21):
+        want[gens] = oracle.bp_run(g, w, gens, R)
+    for depth in DEPTHS:
+        for gens, ref in want.items():
+            with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth) as e:
+                e.init_random(seed)
+                e.step(gens)
+                got = e.store_packed()
+                assert (got == ref).all(), f"depth {depth} gens {gens}"
+                assert e.digest() == oracle.bp_digest(ref, w)
+
+
+@pytest.mark.parametrize("rpw", [16, 32, 48, 100])
+def test_row_blocking(pkg, oracle, rpw):
+    """Many row blocks per strip (rows_per_wave small): block seams exact."""
+    h, w = 300, 4100
+    g = oracle.bp_random(h, w, 5)
+    ref = oracle.bp_run(g, w, 16, oracle.CONWAY)
+    with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw) as e:
+        e.init_random(5)
+        e.step(16)
+        assert (e.store_packed() == ref).all()
+
+
+def test_load_packed_roundtrip(pkg, oracle):
+    h, w = 37, 301
+    rng = np.random.default_rng(1)
+    g = rng.integers(0, 2**63, size=(h, 5), dtype=np.uint64) * 2 + 1
+    with pkg.Engine(h, w, device=0) as e:
+        e.load_packed(g)
+        out = e.store_packed()
+    g[:, 4] &= np.uint64((1 << (301 - 256)) - 1)  # columns >= w are dead
+    assert (out == g).all()
+
+
+def test_ascii_roundtrip_and_errors(pkg, oracle):
+    h, w = 9, 70
+    g = oracle.bp_random(h, w, 11)
+    data = oracle.bp_unpack(g, w)
+    with pkg.Engine(h, w, device=0) as e:
+        e.load_ascii(data)
+        assert e.store_ascii() == data
+        with pytest.raises(pkg.GolError):
+            e.load_ascii(data[:-1])
+        bad = bytearray(data)
+        bad[w] = ord("x")  # line 0 has no '\n' at column w
+        with pytest.raises(pkg.GolError):
+            e.load_ascii(bytes(bad))
+    with pytest.raises(pkg.GolError):
+        pkg.Engine(0, 5, device=0)
+    with pytest.raises(pkg.GolError):
+        pkg.Engine(5, 5, device=0, tb_depth=3)
+
+
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+def test_ref_stripes_conway(pkg, oracle, P):
+    """REF_STRIPES with a rule that gives births (exercises the stripe borders)."""
+    h, w = 203, 190
+    g = oracle.bp_random(h, w, P)
+    ref = oracle.bp_ref_stripes(g, w, 12, P, oracle.CONWAY)
+    with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, semantics=pkg.SEM_REF_STRIPES,
+                    ref_ranks=P, tb_depth=4) as e:
+        e.load_ascii(oracle.bp_unpack(g, w))
+        e.step(12)
+        assert (e.store_packed() == ref).all()
+
+
+# ------------------------------------------------------------ C2: 4096^2
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+def test_c2_4096_per_generation(pkg, oracle, rule):
+    h = w = 4096
+    R = rules(oracle)[rule]
+    g = oracle.bp_random(h, w, 1)
+    with pkg.Engine(h, w, rule=R, device=0) as e:
+        e.init_random(1)
+        assert (e.store_packed() == g).all()
+        for gen in range(1, 17):
+            e.step(1)
+            g = oracle.bp_run(g, w, 1, R, threads=16)
+            assert e.digest() == oracle.bp_digest(g, w), f"gen {gen}"
+        assert (e.store_packed() == g).all()
+
+
+def test_c2_4096_1000_generations_depths_agree(pkg):
+    """Size-independent property: every fused depth gives the same field."""
+    digests = set()
+    for depth in DEPTHS:
+        with pkg.Engine(4096, 4096, rule=(1 << 3, 12), device=0, tb_depth=depth) as e:
+            e.init_random(1)
+            e.step(1000)
+            digests.add(e.digest())
+    assert len(digests) == 1
+
+
+# ------------------------------------------------------------ C3: 65536^2
+@pytest.mark.slow
+def test_c3_65536_vs_oracle(pkg, oracle):
+    h = w = 65536
+    with pkg.Engine(h, w, rule=oracle.CONWAY, device=0) as e:
+        e.init_random(1)
+        e.step(3)
+        got = e.digest()
+    g = oracle.bp_random(h, w, 1)
+    g = oracle.bp_run(g, w, 3, oracle.CONWAY, threads=16)
+    assert got == oracle.bp_digest(g, w)
+
+
+@pytest.mark.slow
+def test_c3_65536_depths_agree(pkg):
+    digests = set()
+    for depth in (1, 8, 16):
+        with pkg.Engine(65536, 65536, rule=(1 << 3, 12), device=0, tb_depth=depth) as e:
+            e.init_random(2)
+            e.step(48)
+            digests.add(e.digest())
+    assert len(digests) == 1
+
+
+# ------------------------------------------------------------ timing API
+def test_timing_counters(pkg):
+    with pkg.Engine(1024, 1024, device=0, tb_depth=8) as e:
+        e.init_random(1)
+        e.set_timing(True)
+        e.step(20)  # 8 + 8 + 4
+        e.sync()
+        t = e.timing()
+    assert t["launches"] == 3
+    assert t["kernel_ms"] > 0
+    assert t["cell_gens"] == 1024 * 1024 * 20
