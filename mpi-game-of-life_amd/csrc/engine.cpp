@@ -197,12 +197,14 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     // choose rows per wavefront: enough wavefronts to fill 256 CUs several times
     int64_t rpw = e->rows_per_wave;
     if (rpw == 0) {
-        rpw = 512;
+        // 128 rows measured best at 65536^2, K = 8 (profiles/); halve while the
+        // launch has fewer than ~2 wavefronts per SIMD (256 CUs x 4 SIMDs)
+        rpw = 128;
         const int64_t min_rpw = std::max<int64_t>(16, 2 * e->K);
         while (rpw > min_rpw) {
             std::vector<SegDesc> t = raw[0];
             finish_segs(t, rpw, e->strips);
-            if (plan_units(t, e->strips) >= 4096) break;
+            if (plan_units(t, e->strips) >= 2048) break;
             rpw /= 2;
         }
     }

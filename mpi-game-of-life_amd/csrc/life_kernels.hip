@@ -58,22 +58,35 @@ struct Stage {
     u2 al;
 };
 
+// v_bitop3_b32: any 3-input bitwise function in one VALU op.  The immediate is
+// the function's truth table evaluated on S0 = 0xF0, S1 = 0xCC, S2 = 0xAA.
+template <uint32_t LUT>
+__device__ __forceinline__ uint32_t lop3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, LUT);
+}
+constexpr uint32_t kXor3 = 0x96;      // a ^ b ^ c
+constexpr uint32_t kMaj = 0xE8;       // majority(a, b, c): carry of a + b + c
+constexpr uint32_t kTwoThree = 0x14;  // (a ^ b) & ~c
+constexpr uint32_t kRefEmit = 0x20;   // a & ~b & c
+constexpr uint32_t kConwayEmit = 0xE0;// a & (b | c)
+
 template <int RULE>
 __device__ __forceinline__ uint32_t rule32(uint32_t as, uint32_t ac, uint32_t bs, uint32_t bc,
                                            uint32_t es, uint32_t ec, uint32_t alive,
                                            uint32_t birth, uint32_t survive)
 {
     // n = A + B + E with A = H3(r-2), B = H2(r-1), E = H3(r): each a 2-bit number.
-    const uint32_t s0 = as ^ bs ^ es;                 // bit 0 of n
-    const uint32_t k0 = (as & bs) | (es & (as ^ bs)); // carry into weight 2
-    const uint32_t p = ac ^ bc ^ ec;                  // weight-2 column sum, bit 0
-    const uint32_t mj = (ac & bc) | (ec & (ac ^ bc)); // weight-2 column sum, carry
+    const uint32_t s0 = lop3<kXor3>(as, bs, es);  // bit 0 of n
+    const uint32_t k0 = lop3<kMaj>(as, bs, es);   // carry into weight 2
+    const uint32_t p = lop3<kXor3>(ac, bc, ec);   // weight-2 column sum, bit 0
+    const uint32_t mj = lop3<kMaj>(ac, bc, ec);   // weight-2 column sum, carry
     // n = s0 + 2*(p + k0) + 4*mj;  n in {2,3}  <=>  mj == 0 && p + k0 == 1
     if constexpr (RULE == RULE_REF) {
         // Parallel_Life_MPI.cpp:47-50: next = alive && n == 2
-        return alive & ~s0 & (p ^ k0) & ~mj;
+        return lop3<kRefEmit>(alive, s0, lop3<kTwoThree>(p, k0, mj));
     } else if constexpr (RULE == RULE_CONWAY) {
-        return (p ^ k0) & ~mj & (s0 | alive);
+        return lop3<kConwayEmit>(lop3<kTwoThree>(p, k0, mj), s0, alive);
     } else {
         const uint32_t n1 = p ^ k0;
         const uint32_t k1 = p & k0;
@@ -110,10 +123,10 @@ __device__ __forceinline__ u2 stage_step(Stage& st, u2 x, uint32_t birth, uint32
     s2.hi = Lhi ^ Rhi;
     c2.lo = Llo & Rlo;
     c2.hi = Lhi & Rhi;
-    s3.lo = s2.lo ^ x.lo;
-    s3.hi = s2.hi ^ x.hi;
-    c3.lo = c2.lo | (s2.lo & x.lo);
-    c3.hi = c2.hi | (s2.hi & x.hi);
+    s3.lo = lop3<kXor3>(Llo, x.lo, Rlo);
+    s3.hi = lop3<kXor3>(Lhi, x.hi, Rhi);
+    c3.lo = lop3<kMaj>(Llo, x.lo, Rlo);
+    c3.hi = lop3<kMaj>(Lhi, x.hi, Rhi);
     u2 y;
     y.lo = rule32<RULE>(st.ps.lo, st.pc.lo, st.hs.lo, st.hc.lo, s3.lo, c3.lo, st.al.lo, birth,
                         survive);
@@ -178,32 +191,57 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     for (int p = 0; p < kPrefetch; ++p) ring[p] = inp[(int64_t)p * a.stride];
     const uint64_t* pf = inp + (int64_t)kPrefetch * a.stride;
 
-    for (int64_t t0 = 0; t0 < T; t0 += kPrefetch) {
+    // input row of step t: dead outside the field / buffer, columns >= w masked
+    auto ingest = [&](int64_t t, uint64_t xv) -> u2 {
+        const int64_t i = row_first + t;
+        const bool ok = (i >= lo_ok) && (i < hi_ok);
+        u2 x;
+        x.lo = ok ? ((uint32_t)xv & cmlo) : 0u;
+        x.hi = ok ? ((uint32_t)(xv >> 32) & cmhi) : 0u;
+        return x;
+    };
+    // stage g (generation g+1) at step t: emits local row row_first + t - (g+1)
+    auto stage = [&](int g, int64_t t, u2 x) -> u2 {
+        x = stage_step<RULE>(st[g], x, a.birth, a.survive);
+        if constexpr (kBirths) {
+            const int64_t r = sg.glob0 + row_first + t - (g + 1);  // field row
+            const bool rok = (r >= 0) && (r < sg.field_h);
+            x.lo = rok ? (x.lo & cmlo) : 0u;
+            x.hi = rok ? (x.hi & cmhi) : 0u;
+        }
+        return x;
+    };
+    auto store = [&](int64_t t, u2 x) {
+        if (t >= 2 * K && t < T && st_lane)
+            outp[(t - 2 * K) * a.stride] = ((uint64_t)x.hi << 32) | x.lo;
+    };
+
+    // Warm-up, fully unrolled: stage g first emits a row that can reach a valid
+    // output at step 2g+2 and needs the two ingests before it, so it runs from
+    // step 2g on; skipping it earlier saves K*(K-1) of the 2K*K warm-up stage steps.
+    constexpr int kWarm = (2 * K + kPrefetch - 1) / kPrefetch * kPrefetch;
+#pragma unroll
+    for (int t = 0; t < kWarm; ++t) {
+        const int p = t % kPrefetch;
+        u2 x = ingest(t, ring[p]);
+        ring[p] = *pf;
+        pf += a.stride;
+#pragma unroll
+        for (int g = 0; g < K; ++g)
+            if (t >= 2 * g) x = stage(g, t, x);
+        if (t >= 2 * K) store(t, x);
+    }
+
+    for (int64_t t0 = kWarm; t0 < T; t0 += kPrefetch) {
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
             const int64_t t = t0 + p;
-            const int64_t i = row_first + t;  // incoming local row
-            uint64_t xv = ring[p];
+            u2 x = ingest(t, ring[p]);
             ring[p] = *pf;
             pf += a.stride;
-            const bool ok = (i >= lo_ok) && (i < hi_ok);
-            u2 x;
-            x.lo = ok ? ((uint32_t)xv & cmlo) : 0u;
-            x.hi = ok ? ((uint32_t)(xv >> 32) & cmhi) : 0u;
 #pragma unroll
-            for (int g = 0; g < K; ++g) {
-                x = stage_step<RULE>(st[g], x, a.birth, a.survive);
-                if constexpr (kBirths) {
-                    // emitted row i-(g+1): dead outside the field and beyond column w
-                    const int64_t r = i - (g + 1);
-                    const bool rok = (sg.glob0 + r >= 0) && (sg.glob0 + r < sg.field_h);
-                    x.lo = rok ? (x.lo & cmlo) : 0u;
-                    x.hi = rok ? (x.hi & cmhi) : 0u;
-                }
-            }
-            if (t >= 2 * K && t < T && st_lane) {
-                outp[(t - 2 * K) * a.stride] = ((uint64_t)x.hi << 32) | x.lo;
-            }
+            for (int g = 0; g < K; ++g) x = stage(g, t, x);
+            store(t, x);
         }
     }
 }
