@@ -147,6 +147,17 @@ gol_status gol_comm_unique_id(uint8_t id[128]);
 gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int rank,
                            int nranks, const uint8_t id[128], gol_engine** out);
 
+/* ---- Multi-GPU (or multi-stripe) inside ONE process, no RCCL ----
+ * `nranks` stripe engines of one GLOBAL field (the same partition and halo
+ * rounds as gol_create_rank), stripe r on devices[r] (NULL = cfg->device for
+ * all; repeats allowed, so several stripes can share one GPU).  Halos move by
+ * device-to-device / xGMI peer copies ordered with HIP events.  Members are
+ * loaded, stored and digested one by one like rank engines, advanced together
+ * by gol_group_step, and destroyed with gol_destroy. */
+gol_status gol_create_group(uint64_t h, uint64_t w, const gol_config* cfg, int nranks,
+                            const int* devices, gol_engine** engines);
+gol_status gol_group_step(gol_engine** engines, int nranks, uint64_t generations);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,7 +28,7 @@ EXPORTS = [
     "gol_load_packed", "gol_store_packed", "gol_init_random", "gol_step", "gol_sync",
     "gol_digest", "gol_destroy", "gol_last_error", "gol_set_timing", "gol_get_timing",
     "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
-    "gol_create_rank",
+    "gol_create_rank", "gol_create_group", "gol_group_step",
 ]
 
 
@@ -109,10 +109,14 @@ def lib():
     L.gol_info.argtypes = [vp, pu64, pu64, pu64, pu64, ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.gol_rank_rows.argtypes = [u64, i32, i32, pu64, pu64]
     L.gol_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.gol_create_group.argtypes = [u64, u64, ctypes.POINTER(Config), i32,
+                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp)]
+    L.gol_group_step.argtypes = [ctypes.POINTER(vp), i32, u64]
     for name in ["gol_create", "gol_create_rank", "gol_load_ascii", "gol_store_ascii",
                  "gol_load_packed", "gol_store_packed", "gol_init_random", "gol_step",
                  "gol_sync", "gol_digest", "gol_set_timing", "gol_get_timing",
-                 "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id"]:
+                 "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
+                 "gol_create_group", "gol_group_step"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -153,13 +157,16 @@ class Engine:
     """One field (or one rank's stripe of it) resident on one GPU."""
 
     def __init__(self, h, w, rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1,
-                 tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None):
+                 tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None,
+                 _handle=None):
         self.h, self.w = h, w
         self.wq = (w + 63) // 64
         cfg = make_config(rule, device, semantics, ref_ranks, tb_depth, halo_depth,
                           rows_per_wave)
         handle = ctypes.c_void_p()
-        if rank is None:
+        if _handle is not None:
+            handle = _handle
+        elif rank is None:
             _check(lib().gol_create(h, w, ctypes.byref(cfg), ctypes.byref(handle)))
         else:
             if uid is None or len(uid) != 128:
@@ -236,3 +243,65 @@ class Engine:
         _check(lib().gol_get_timing(self._h, ctypes.byref(t)))
         return {"launches": t.launches, "kernel_ms": t.kernel_ms, "cell_gens": t.cell_gens,
                 "cell_gens_computed": t.cell_gens_computed}
+
+
+class Group:
+    """`nranks` stripe engines of one field in this process (gol_create_group):
+    the multi-GPU partition/halo logic with device-copy transport; stripes may
+    share a GPU."""
+
+    def __init__(self, h, w, nranks, devices=None, rule=REF_RULE, tb_depth=0, halo_depth=0,
+                 rows_per_wave=0):
+        self.h, self.w, self.n = h, w, nranks
+        cfg = make_config(rule, -1 if devices else 0, SEM_GLOBAL, 1, tb_depth, halo_depth,
+                          rows_per_wave)
+        hs = (ctypes.c_void_p * nranks)()
+        devs = (ctypes.c_int * nranks)(*(devices or [0] * nranks))
+        _check(lib().gol_create_group(h, w, ctypes.byref(cfg), nranks, devs, hs))
+        self._hs = hs
+        self.members = [Engine(h, w, _handle=ctypes.c_void_p(hs[r])) for r in range(nranks)]
+
+    def close(self):
+        for m in self.members:
+            m.close()
+        self.members = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def step(self, gens):
+        _check(lib().gol_group_step(self._hs, self.n, gens))
+
+    def sync(self):
+        for m in self.members:
+            m.sync()
+
+    def init_random(self, seed=1):
+        for m in self.members:
+            m.init_random(seed)
+
+    def load_packed(self, arr):
+        for m in self.members:
+            m.load_packed(arr[m.row0:m.row0 + m.rows])
+
+    def load_ascii(self, data: bytes):
+        for m in self.members:
+            m.load_ascii(data[m.row0 * (self.w + 1):(m.row0 + m.rows) * (self.w + 1)])
+
+    def store_packed(self):
+        import numpy as np
+        return np.concatenate([m.store_packed() for m in self.members])
+
+    def store_ascii(self) -> bytes:
+        return b"".join(m.store_ascii() for m in self.members)
+
+    def digest(self):
+        live = hsh = 0
+        for m in self.members:
+            a, b = m.digest()
+            live += a
+            hsh = (hsh + b) & 0xFFFFFFFFFFFFFFFF
+        return live, hsh

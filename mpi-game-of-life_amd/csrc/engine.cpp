@@ -145,6 +145,12 @@ struct gol_engine {
     uint64_t row0 = 0, R = 0, Hx = 0;
     ncclComm_t comm = nullptr;
 
+    // in-process group (gol_create_group): halo exchange by device copies
+    gol_engine* up = nullptr;
+    gol_engine* down = nullptr;
+    bool grouped = false;
+    hipEvent_t ev_ready = nullptr, ev_copied = nullptr;
+
     uint64_t buf_rows = 0;
     uint64_t* alloc[2] = {nullptr, nullptr};
     uint64_t* buf[2] = {nullptr, nullptr};
@@ -486,10 +492,14 @@ gol_status gol_comm_unique_id(uint8_t id[128])
     return GOL_OK;
 }
 
-gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
-                           const uint8_t id[128], gol_engine** out)
+}  // extern "C"
+
+namespace {
+
+// Geometry + device state of stripe `rank` of `nranks` (no transport yet).
+gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
+                            gol_engine** out)
 {
-    if (!out || !id) return fail(GOL_EINVAL, "null argument");
     *out = nullptr;
     gol_status st = check_cfg(cfg);
     if (st != GOL_OK) return st;
@@ -499,6 +509,8 @@ gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int ra
     uint64_t row0, rows;
     st = gol_rank_rows(h, nranks, rank, &row0, &rows);
     if (st != GOL_OK) return st;
+    const uint64_t minR = h / (uint64_t)nranks;
+    if (minR == 0) return fail(GOL_EINVAL, "fewer rows than ranks");
     gol_engine* e = new (std::nothrow) gol_engine();
     if (!e) return fail(GOL_ENOMEM, "host allocation");
     e->rank = rank;
@@ -506,28 +518,11 @@ gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int ra
     e->row0 = row0;
     e->R = rows;
     const uint32_t K = cfg->tb_depth ? cfg->tb_depth : 8;
-    uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 4 * (uint64_t)K;
-    // a rank sends its first/last Hx own rows: every rank needs R >= Hx
-    const uint64_t minR = h / (uint64_t)nranks;
-    if (Hx > minR) Hx = minR;
-    if (Hx == 0) {
-        delete e;
-        return fail(GOL_EINVAL, "fewer rows than ranks");
-    }
+    // rounds of halo_depth generations between exchanges (default 8 launches)
+    uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 8 * (uint64_t)K;
+    if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
     e->Hx = nranks > 1 ? Hx : 0;
-    if (nranks > 1) {
-        st = init_common(e, h, w, cfg);
-        if (st == GOL_OK) {
-            ncclUniqueId u;
-            std::memcpy(&u, id, 128);
-            ncclResult_t r = ncclCommInitRank(&e->comm, nranks, u, rank);
-            if (r != ncclSuccess)
-                st = fail(GOL_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-        }
-    } else {
-        gol_config c1 = *cfg;
-        st = init_common(e, h, w, &c1);
-    }
+    st = init_common(e, h, w, cfg);
     if (st != GOL_OK) {
         std::string msg = g_last_error;
         gol_destroy(e);
@@ -538,11 +533,83 @@ gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int ra
     return GOL_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
+                           const uint8_t id[128], gol_engine** out)
+{
+    if (!out || !id) return fail(GOL_EINVAL, "null argument");
+    gol_engine* e = nullptr;
+    gol_status st = make_rank_engine(h, w, cfg, rank, nranks, &e);
+    if (st != GOL_OK) return st;
+    if (nranks > 1) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, 128);
+        ncclResult_t r = ncclCommInitRank(&e->comm, nranks, u, rank);
+        if (r != ncclSuccess) {
+            gol_destroy(e);
+            return fail(GOL_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+    }
+    *out = e;
+    return GOL_OK;
+}
+
+gol_status gol_create_group(uint64_t h, uint64_t w, const gol_config* cfg, int nranks,
+                            const int* devices, gol_engine** engines)
+{
+    if (!engines || nranks <= 0) return fail(GOL_EINVAL, "bad group arguments");
+    for (int r = 0; r < nranks; ++r) engines[r] = nullptr;
+    gol_status st = GOL_OK;
+    for (int r = 0; r < nranks && st == GOL_OK; ++r) {
+        gol_config c = *cfg;
+        c.device = devices ? devices[r] : (cfg->device >= 0 ? cfg->device : -1);
+        st = make_rank_engine(h, w, &c, r, nranks, &engines[r]);
+    }
+    for (int r = 0; r < nranks && st == GOL_OK; ++r) {
+        gol_engine* e = engines[r];
+        e->grouped = nranks > 1;
+        e->up = r > 0 ? engines[r - 1] : nullptr;
+        e->down = r + 1 < nranks ? engines[r + 1] : nullptr;
+        hipError_t he = hipSetDevice(e->device);
+        if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_ready, hipEventDisableTiming);
+        if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_copied, hipEventDisableTiming);
+        for (gol_engine* n : {e->up, e->down}) {
+            if (he != hipSuccess || !n || n->device == e->device) continue;
+            int can = 0;
+            he = hipDeviceCanAccessPeer(&can, e->device, n->device);
+            if (he == hipSuccess && can) {
+                he = hipDeviceEnablePeerAccess(n->device, 0);
+                if (he == hipErrorPeerAccessAlreadyEnabled) {
+                    (void)hipGetLastError();
+                    he = hipSuccess;
+                }
+            }
+        }
+        if (he != hipSuccess) st = fail(GOL_EHIP, std::string("group setup: ") + hipGetErrorString(he));
+    }
+    if (st != GOL_OK) {
+        std::string msg = g_last_error;
+        for (int r = 0; r < nranks; ++r) {
+            gol_destroy(engines[r]);
+            engines[r] = nullptr;
+        }
+        g_last_error = msg;
+    }
+    return st;
+}
+
 void gol_destroy(gol_engine* e)
 {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
+    if (e->up) e->up->down = nullptr;
+    if (e->down) e->down->up = nullptr;
+    if (e->ev_ready) (void)hipEventDestroy(e->ev_ready);
+    if (e->ev_copied) (void)hipEventDestroy(e->ev_copied);
     for (auto& p : e->plans)
         if (p.dev) (void)hipFree(p.dev);
     for (int b = 0; b < 2; ++b)
@@ -656,23 +723,68 @@ gol_status gol_init_random(gol_engine* e, uint64_t seed)
     return GOL_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// The launches of one round of `round` generations after a halo exchange: each
+// launch of depth d shrinks the valid region by d rows per side (plan c-1 for a
+// cumulative shrink of c).
+gol_status run_round(gol_engine* e, uint64_t round)
+{
+    uint64_t done = 0;
+    while (done < round) {
+        const uint32_t d = pick_depth(e->K, round - done);
+        done += d;
+        gol_status st = launch(e, (int)(done - 1), d);
+        if (st != GOL_OK) return st;
+    }
+    return GOL_OK;
+}
+
+// Loopback exchange of a group member: pull the neighbours' boundary rows into
+// this engine's halo rows (same layout as the RCCL exchange).
+gol_status pull_halos(gol_engine* e)
+{
+    const size_t S = e->stride, n = (size_t)e->Hx * S * sizeof(uint64_t);
+    uint64_t* b = e->buf[e->cur];
+    if (gol_engine* u = e->up) {
+        HIP_TRY(hipStreamWaitEvent(e->stream, u->ev_ready, 0));
+        const uint64_t* src = u->buf[u->cur] + u->R * S;  // its last Hx own rows
+        if (u->device == e->device)
+            HIP_TRY(hipMemcpyAsync(b, src, n, hipMemcpyDeviceToDevice, e->stream));
+        else
+            HIP_TRY(hipMemcpyPeerAsync(b, e->device, src, u->device, n, e->stream));
+    }
+    if (gol_engine* d = e->down) {
+        HIP_TRY(hipStreamWaitEvent(e->stream, d->ev_ready, 0));
+        const uint64_t* src = d->buf[d->cur] + d->Hx * S;  // its first Hx own rows
+        uint64_t* dst = b + (e->R + e->Hx) * S;
+        if (d->device == e->device)
+            HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, e->stream));
+        else
+            HIP_TRY(hipMemcpyPeerAsync(dst, e->device, src, d->device, n, e->stream));
+    }
+    HIP_TRY(hipEventRecord(e->ev_copied, e->stream));
+    return GOL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 gol_status gol_step(gol_engine* e, uint64_t generations)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
+    if (e->grouped) return fail(GOL_ESTATE, "group members advance with gol_group_step");
     HIP_TRY(hipSetDevice(e->device));
     uint64_t left = generations;
     if (e->nranks > 1) {
         while (left > 0) {
             const uint64_t round = std::min<uint64_t>(left, e->Hx);
             gol_status st = exchange(e);
+            if (st == GOL_OK) st = run_round(e, round);
             if (st != GOL_OK) return st;
-            uint64_t done = 0;
-            while (done < round) {
-                const uint32_t d = pick_depth(e->K, round - done);
-                done += d;
-                st = launch(e, (int)(done - 1), d);
-                if (st != GOL_OK) return st;
-            }
             left -= round;
         }
         return GOL_OK;
@@ -682,6 +794,42 @@ gol_status gol_step(gol_engine* e, uint64_t generations)
         gol_status st = launch(e, 0, d);
         if (st != GOL_OK) return st;
         left -= d;
+    }
+    return GOL_OK;
+}
+
+gol_status gol_group_step(gol_engine** engines, int nranks, uint64_t generations)
+{
+    if (!engines || nranks <= 0) return fail(GOL_EINVAL, "bad group arguments");
+    for (int r = 0; r < nranks; ++r) {
+        gol_engine* e = engines[r];
+        if (!e || e->rank != r || e->nranks != nranks)
+            return fail(GOL_EINVAL, "engines must be the members of one group, in rank order");
+    }
+    if (nranks == 1) return gol_step(engines[0], generations);
+    const uint64_t Hx = engines[0]->Hx;
+    uint64_t left = generations;
+    while (left > 0) {
+        const uint64_t round = std::min<uint64_t>(left, Hx);
+        for (int r = 0; r < nranks; ++r) {  // every member's state is final
+            gol_engine* e = engines[r];
+            HIP_TRY(hipSetDevice(e->device));
+            HIP_TRY(hipEventRecord(e->ev_ready, e->stream));
+        }
+        for (int r = 0; r < nranks; ++r) {
+            HIP_TRY(hipSetDevice(engines[r]->device));
+            gol_status st = pull_halos(engines[r]);
+            if (st != GOL_OK) return st;
+        }
+        for (int r = 0; r < nranks; ++r) {  // neighbours done reading my rows
+            gol_engine* e = engines[r];
+            HIP_TRY(hipSetDevice(e->device));
+            if (e->up) HIP_TRY(hipStreamWaitEvent(e->stream, e->up->ev_copied, 0));
+            if (e->down) HIP_TRY(hipStreamWaitEvent(e->stream, e->down->ev_copied, 0));
+            gol_status st = run_round(e, round);
+            if (st != GOL_OK) return st;
+        }
+        left -= round;
     }
     return GOL_OK;
 }

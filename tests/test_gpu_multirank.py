@@ -1,0 +1,79 @@
+"""GPU parity of the multi-stripe path (row stripes + k-deep halo rounds).
+
+gol_create_group runs the same partition (gol_rank_rows), halo layout and
+shrinking launch rounds as the RCCL rank engines (gol_create_rank), with the
+halo rows moved by device copies, so every stripe count can be checked on one
+GPU against the oracle's single-field evolution.
+"""
+import hashlib
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4, 8])
+@pytest.mark.parametrize("rule", ["ref", "conway", "highlife"])
+def test_group_matches_single_field(pkg, oracle, nranks, rule):
+    R = {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}[rule]
+    h, w = 203, 4000
+    g = oracle.bp_random(h, w, 3 + nranks)
+    for tb, hx, gens in ((8, 0, 37), (4, 12, 30), (2, 5, 11), (1, 3, 7), (16, 16, 33)):
+        ref = oracle.bp_run(g, w, gens, R)
+        with pkg.Group(h, w, nranks, rule=R, tb_depth=tb, halo_depth=hx) as grp:
+            grp.load_packed(g)
+            grp.step(gens)
+            grp.sync()
+            got = grp.store_packed()
+            assert (got == ref).all(), f"tb {tb} hx {hx} gens {gens}"
+            assert grp.digest() == oracle.bp_digest(ref, w)
+
+
+def test_group_reference_data(pkg, ref_data):
+    """Intended semantics of the reference (its halo exchange actually working)
+    == the reference's own -np 1 output."""
+    gold = json.load(open(os.path.join(GOLDEN, "ref_outputs.json")))
+    h, w = gold["h"], gold["w"]
+    for case in gold["cases"]:
+        if case["np"] != 1 or case["gens"] not in (1, 2, 3, 4, 100):
+            continue
+        with pkg.Group(h, w, 4) as grp:
+            grp.load_ascii(ref_data)
+            grp.step(case["gens"])
+            out = grp.store_ascii()
+        assert hashlib.sha256(out).hexdigest() == case["sha256"], case
+
+
+def test_group_large_equals_single(pkg):
+    """Size-independent property at the per-GPU shape of 8-way 65536^2 runs."""
+    h, w = 16384, 65536
+    with pkg.Engine(h, w, rule=pkg.CONWAY, device=0) as e:
+        e.init_random(9)
+        e.step(100)
+        want = e.digest()
+    with pkg.Group(h, w, 8, rule=pkg.CONWAY) as grp:
+        grp.init_random(9)
+        grp.step(100)
+        assert grp.digest() == want
+
+
+def test_grouped_engine_refuses_solo_step(pkg):
+    with pkg.Group(64, 64, 2) as grp:
+        with pytest.raises(pkg.GolError) as ei:
+            grp.members[0].step(1)
+        assert ei.value.status == pkg.GOL_ESTATE
+
+
+def test_rank_engine_single_rank(pkg, oracle):
+    """gol_create_rank with nranks = 1 (no communicator) is a plain field."""
+    h, w = 100, 130
+    g = oracle.bp_random(h, w, 4)
+    with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, rank=0, nranks=1,
+                    uid=pkg.unique_id()) as e:
+        e.load_packed(g)
+        e.step(20)
+        assert (e.store_packed() == oracle.bp_run(g, w, 20, oracle.CONWAY)).all()
