@@ -68,11 +68,14 @@ typedef struct gol_config {
     uint32_t semantics;    /* gol_semantics */
     uint32_t ref_ranks;    /* P for GOL_SEM_REF_STRIPES (must satisfy h >= P) */
     uint32_t tb_depth;     /* generations fused per kernel launch (temporal
-                              blocking); 0 = auto; allowed 1,2,4,8,16 */
+                              blocking); 0 = auto; allowed 1,2,4,6,7,8,12,16 */
     uint32_t halo_depth;   /* multi-rank: halo rows exchanged per round
                               (= generations between exchanges); 0 = auto */
     uint32_t rows_per_wave;/* rows each wavefront streams per launch; 0 = auto */
-    uint32_t reserved[4];
+    uint32_t kernel_variant;/* stencil state layout: 0 = auto, 1 = full (14 VGPRs
+                              per fused generation), 2 = compact (10 VGPRs, +4 VALU
+                              ops per word-generation) */
+    uint32_t reserved[3];
 } gol_config;
 
 typedef struct gol_engine gol_engine;

@@ -48,7 +48,8 @@ class Config(ctypes.Structure):
         ("tb_depth", ctypes.c_uint32),
         ("halo_depth", ctypes.c_uint32),
         ("rows_per_wave", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 4),
+        ("kernel_variant", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 3),
     ]
 
 
@@ -128,7 +129,7 @@ def _check(st):
 
 
 def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_depth=0,
-                halo_depth=0, rows_per_wave=0):
+                halo_depth=0, rows_per_wave=0, kernel_variant=0):
     c = Config()
     lib().gol_config_init(ctypes.byref(c))
     c.birth_mask, c.survive_mask = rule
@@ -138,6 +139,7 @@ def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_
     c.tb_depth = tb_depth
     c.halo_depth = halo_depth
     c.rows_per_wave = rows_per_wave
+    c.kernel_variant = kernel_variant
     return c
 
 
@@ -158,11 +160,11 @@ class Engine:
 
     def __init__(self, h, w, rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1,
                  tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None,
-                 _handle=None):
+                 kernel_variant=0, _handle=None):
         self.h, self.w = h, w
         self.wq = (w + 63) // 64
         cfg = make_config(rule, device, semantics, ref_ranks, tb_depth, halo_depth,
-                          rows_per_wave)
+                          rows_per_wave, kernel_variant)
         handle = ctypes.c_void_p()
         if _handle is not None:
             handle = _handle
@@ -251,10 +253,10 @@ class Group:
     share a GPU."""
 
     def __init__(self, h, w, nranks, devices=None, rule=REF_RULE, tb_depth=0, halo_depth=0,
-                 rows_per_wave=0):
+                 rows_per_wave=0, kernel_variant=0):
         self.h, self.w, self.n = h, w, nranks
         cfg = make_config(rule, -1 if devices else 0, SEM_GLOBAL, 1, tb_depth, halo_depth,
-                          rows_per_wave)
+                          rows_per_wave, kernel_variant)
         hs = (ctypes.c_void_p * nranks)()
         devs = (ctypes.c_int * nranks)(*(devices or [0] * nranks))
         _check(lib().gol_create_group(h, w, ctypes.byref(cfg), nranks, devs, hs))

@@ -45,7 +45,6 @@ gol_status fail(gol_status st, const std::string& msg)
             return fail(GOL_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(_r));     \
     } while (0)
 
-constexpr uint32_t kDepths[] = {16, 8, 4, 2, 1};
 
 uint64_t last_mask(uint64_t w)
 {
@@ -137,6 +136,7 @@ struct gol_engine {
     gol::RuleKind rule = gol::RULE_REF;
     uint32_t K = 8;
     uint32_t rows_per_wave = 0;
+    bool compact = false;
     uint32_t sem = GOL_SEM_GLOBAL;
     uint32_t P = 1;
 
@@ -233,9 +233,10 @@ gol_status check_cfg(const gol_config* cfg)
     if (!cfg) return fail(GOL_EINVAL, "null config");
     if (cfg->birth_mask >= 512 || cfg->survive_mask >= 512)
         return fail(GOL_EINVAL, "rule masks must be 9-bit");
-    if (cfg->tb_depth != 0 && cfg->tb_depth != 1 && cfg->tb_depth != 2 && cfg->tb_depth != 4 &&
-        cfg->tb_depth != 8 && cfg->tb_depth != 16)
-        return fail(GOL_EINVAL, "tb_depth must be 0 (auto), 1, 2, 4, 8 or 16");
+    if (cfg->tb_depth != 0 && std::find(std::begin(gol::kDepthList), std::end(gol::kDepthList),
+                                        (int)cfg->tb_depth) == std::end(gol::kDepthList))
+        return fail(GOL_EINVAL, "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16");
+    if (cfg->kernel_variant > 2) return fail(GOL_EINVAL, "kernel_variant must be 0, 1 or 2");
     if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
     return GOL_OK;
 }
@@ -258,6 +259,7 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->rule = gol::RULE_GENERIC;
     e->K = cfg->tb_depth ? cfg->tb_depth : 8;
     e->rows_per_wave = cfg->rows_per_wave;
+    e->compact = cfg->kernel_variant == 2;
     e->sem = cfg->semantics;
     e->strips = (int32_t)((e->wq + gol::kStripOut - 1) / gol::kStripOut);
 
@@ -391,7 +393,7 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth)
         if (st != GOL_OK) return st;
         HIP_TRY(hipEventRecord(e0, e->stream));
     }
-    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->stream));
+    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->compact, e->stream));
     if (e->timing) {
         HIP_TRY(hipEventRecord(e1, e->stream));
         e->ev_pending.push_back({e0, e1});
@@ -407,8 +409,8 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth)
 
 uint32_t pick_depth(uint32_t K, uint64_t remaining)
 {
-    for (uint32_t d : kDepths)
-        if (d <= K && d <= remaining) return d;
+    for (int d : gol::kDepthList)
+        if ((uint32_t)d <= K && (uint64_t)d <= remaining) return (uint32_t)d;
     return 1;
 }
 

@@ -52,8 +52,12 @@ struct StepArgs {
     uint32_t birth, survive;
 };
 
-// Launch `depth` fused generations (depth in {1,2,4,8,16}).
-hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, hipStream_t s);
+// Fused depths with an instantiated kernel, largest first.
+constexpr int kDepthList[] = {16, 12, 8, 7, 6, 4, 2, 1};
+
+// Launch `depth` fused generations (depth in kDepthList); `compact` selects the
+// 10-dword stage state (more waves per SIMD, 4 more VALU ops per word-generation).
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, bool compact, hipStream_t s);
 
 // Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field
 // rows [glob_row0, glob_row0+nrows).

@@ -142,9 +142,55 @@ __device__ __forceinline__ u2 stage_step(Stage& st, u2 x, uint32_t birth, uint32
     return y;
 }
 
+// Compact stage state (10 dwords instead of 14): H3 of row r-2, H2 and cells of
+// row r-1; H3(r-1) = H2(r-1) + cells(r-1) is rebuilt (2 ops per half) when the
+// window shifts.  Trades 4 VALU ops per word-generation for 4 VGPRs per stage,
+// i.e. occupancy at larger K.
+struct StageC {
+    u2 ps, pc;
+    u2 hs, hc;
+    u2 al;
+};
+constexpr uint32_t kOrAnd = 0xF8;  // a | (b & c)
+
+template <int RULE>
+__device__ __forceinline__ u2 stage_step(StageC& st, u2 x, uint32_t birth, uint32_t survive)
+{
+    const uint32_t lh = lane_from_left(x.hi);
+    const uint32_t rl = lane_from_right(x.lo);
+    const uint32_t Llo = __builtin_amdgcn_alignbit(x.lo, lh, 31);
+    const uint32_t Lhi = __builtin_amdgcn_alignbit(x.hi, x.lo, 31);
+    const uint32_t Rlo = __builtin_amdgcn_alignbit(x.hi, x.lo, 1);
+    const uint32_t Rhi = __builtin_amdgcn_alignbit(rl, x.hi, 1);
+    u2 y;
+    y.lo = rule32<RULE>(st.ps.lo, st.pc.lo, st.hs.lo, st.hc.lo, lop3<kXor3>(Llo, x.lo, Rlo),
+                        lop3<kMaj>(Llo, x.lo, Rlo), st.al.lo, birth, survive);
+    y.hi = rule32<RULE>(st.ps.hi, st.pc.hi, st.hs.hi, st.hc.hi, lop3<kXor3>(Lhi, x.hi, Rhi),
+                        lop3<kMaj>(Lhi, x.hi, Rhi), st.al.hi, birth, survive);
+    st.ps.lo = st.hs.lo ^ st.al.lo;
+    st.ps.hi = st.hs.hi ^ st.al.hi;
+    st.pc.lo = lop3<kOrAnd>(st.hc.lo, st.hs.lo, st.al.lo);
+    st.pc.hi = lop3<kOrAnd>(st.hc.hi, st.hs.hi, st.al.hi);
+    st.hs.lo = Llo ^ Rlo;
+    st.hs.hi = Lhi ^ Rhi;
+    st.hc.lo = Llo & Rlo;
+    st.hc.hi = Lhi & Rhi;
+    st.al = x;
+    return y;
+}
+
+template <bool COMPACT>
+struct StageOf {
+    using type = Stage;
+};
+template <>
+struct StageOf<true> {
+    using type = StageC;
+};
+
 constexpr int kPrefetch = 4;
 
-template <int K, int RULE>
+template <int K, int RULE, bool COMPACT>
 __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 {
     constexpr bool kBirths = RULE != RULE_REF;
@@ -180,11 +226,9 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     const int64_t lo_ok = max((int64_t)0, -sg.glob0);             // first local row in field
     const int64_t hi_ok = min(sg.in_rows, sg.field_h - sg.glob0);  // one past last
 
-    Stage st[K];
+    typename StageOf<COMPACT>::type st[K];
 #pragma unroll
-    for (int g = 0; g < K; ++g) {
-        st[g].ps = st[g].pc = st[g].cs = st[g].cc = st[g].hs = st[g].hc = st[g].al = u2{0u, 0u};
-    }
+    for (int g = 0; g < K; ++g) st[g] = {};
 
     uint64_t ring[kPrefetch];
 #pragma unroll
@@ -246,23 +290,29 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     }
 }
 
-template <int K>
+template <int K, bool COMPACT>
 hipError_t launch_depth(const StepArgs& a, RuleKind rule, hipStream_t s)
 {
     const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
     const dim3 block(64 * kWavesPerBlock);
     switch (rule) {
     case RULE_REF:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, COMPACT>), grid, block, 0, s, a);
         break;
     case RULE_CONWAY:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, COMPACT>), grid, block, 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, COMPACT>), grid, block, 0, s, a);
         break;
     }
     return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_variant(const StepArgs& a, RuleKind rule, bool compact, hipStream_t s)
+{
+    return compact ? launch_depth<K, true>(a, rule, s) : launch_depth<K, false>(a, rule, s);
 }
 
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t idx)
@@ -318,15 +368,18 @@ __global__ __launch_bounds__(256) void digest_kernel(const uint64_t* buf, int64_
 
 }  // namespace
 
-hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, hipStream_t s)
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, bool compact, hipStream_t s)
 {
     if (a.total_units <= 0) return hipSuccess;
     switch (depth) {
-    case 1: return launch_depth<1>(a, rule, s);
-    case 2: return launch_depth<2>(a, rule, s);
-    case 4: return launch_depth<4>(a, rule, s);
-    case 8: return launch_depth<8>(a, rule, s);
-    case 16: return launch_depth<16>(a, rule, s);
+    case 1: return launch_variant<1>(a, rule, compact, s);
+    case 2: return launch_variant<2>(a, rule, compact, s);
+    case 4: return launch_variant<4>(a, rule, compact, s);
+    case 6: return launch_variant<6>(a, rule, compact, s);
+    case 7: return launch_variant<7>(a, rule, compact, s);
+    case 8: return launch_variant<8>(a, rule, compact, s);
+    case 12: return launch_variant<12>(a, rule, compact, s);
+    case 16: return launch_variant<16>(a, rule, compact, s);
     default: return hipErrorInvalidValue;
     }
 }

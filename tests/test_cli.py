@@ -1,0 +1,82 @@
+"""The `gol` CLI reproduces the reference program's surface (Parallel_Life_MPI.cpp
+main :190-240): same input files, same output.txt bytes and offsets (not
+truncated, :166-170), same stdout lines (:179, :236)."""
+import hashlib
+import json
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN
+
+GOLD = json.load(open(os.path.join(GOLDEN, "ref_outputs.json")))
+
+
+def setup_dir(tmp_path, epochs, h=1500, w=500, data=None):
+    shutil.copy(os.path.join(GOLDEN, "data.txt"), tmp_path / "data.txt")
+    if data is not None:
+        (tmp_path / "data.txt").write_bytes(data)
+    (tmp_path / "grid_size_data.txt").write_text(f"{h} {w} {epochs}")
+    return tmp_path
+
+
+def run_cli(pkg, d, *args):
+    return subprocess.run([pkg.CLI_PATH, "--dir", str(d), *args], capture_output=True,
+                          text=True, timeout=300)
+
+
+def test_zero_epochs_echo_and_no_truncate(pkg, tmp_path):
+    """E = 0 needs no GPU: the reference writes the input bytes back; a longer
+    pre-existing output.txt keeps its tail (no O_TRUNC)."""
+    d = setup_dir(tmp_path, 0)
+    stale = b"x" * (1500 * 501 + 37)
+    (d / "output.txt").write_bytes(stale)
+    r = run_cli(pkg, d, "--ref-ranks", "3")
+    assert r.returncode == 0, r.stderr
+    out = (d / "output.txt").read_bytes()
+    assert out[:1500 * 501] == (d / "data.txt").read_bytes()
+    assert out[1500 * 501:] == b"x" * 37
+    lines = r.stdout.splitlines()
+    assert lines[:3] == [f"Process {i} wrote data to the file." for i in range(3)]
+    assert re.fullmatch(r"Total time = [0-9.e+-]+", lines[3])
+
+
+def test_bad_config_file(pkg, tmp_path):
+    (tmp_path / "grid_size_data.txt").write_text("12 x")
+    r = run_cli(pkg, tmp_path)
+    assert r.returncode == 1
+    assert "Error reading integers from file." in r.stderr
+
+
+def test_short_data_file(pkg, tmp_path):
+    d = setup_dir(tmp_path, 0, data=b"0101\n")
+    r = run_cli(pkg, d)
+    assert r.returncode == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("np_,gens", [(1, 100), (4, 100), (2, 3), (8, 4)])
+def test_cli_matches_reference_output(pkg, tmp_path, np_, gens):
+    case = [c for c in GOLD["cases"] if c["np"] == np_ and c["gens"] == gens][0]
+    d = setup_dir(tmp_path, gens)
+    args = ["--ref-ranks", str(np_)] if np_ > 1 else []
+    r = run_cli(pkg, d, *args)
+    assert r.returncode == 0, r.stderr
+    out = (d / "output.txt").read_bytes()
+    assert hashlib.sha256(out).hexdigest() == case["sha256"]
+    assert len(r.stdout.splitlines()) == np_ + 1
+
+
+@pytest.mark.gpu
+def test_cli_conway_rule(pkg, oracle, tmp_path):
+    h, w = 50, 70
+    g = oracle.bp_random(h, w, 2)
+    data = oracle.bp_unpack(g, w)
+    d = setup_dir(tmp_path, 9, h, w, data)
+    r = run_cli(pkg, d, "--rule", "B3/S23")
+    assert r.returncode == 0, r.stderr
+    assert (d / "output.txt").read_bytes() == oracle.bp_unpack(
+        oracle.bp_run(g, w, 9, oracle.CONWAY), w)

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 GOLD = json.load(open(os.path.join(GOLDEN, "ref_outputs.json")))
 H, W = GOLD["h"], GOLD["w"]
-DEPTHS = [1, 2, 4, 8, 16]
+DEPTHS = [1, 2, 4, 6, 7, 8, 12, 16]
 
 
 def rules(oracle):
@@ -75,13 +75,14 @@ def test_random_fields_every_depth(pkg, oracle, shape, rule):
     g = oracle.bp_random(h, w, seed)
     for gens in (1, 3, 16, 21):
         want[gens] = oracle.bp_run(g, w, gens, R)
-    for depth in DEPTHS:
+    for depth, variant in [(d, v) for d in DEPTHS for v in (1, 2)]:
         for gens, ref in want.items():
-            with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth) as e:
+            with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth,
+                            kernel_variant=variant) as e:
                 e.init_random(seed)
                 e.step(gens)
                 got = e.store_packed()
-                assert (got == ref).all(), f"depth {depth} gens {gens}"
+                assert (got == ref).all(), f"depth {depth} variant {variant} gens {gens}"
                 assert e.digest() == oracle.bp_digest(ref, w)
 
 

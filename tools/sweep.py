@@ -22,6 +22,7 @@ def main():
     p.add_argument("--gens", type=int, default=96)
     p.add_argument("--depths", default="4,8,16")
     p.add_argument("--rpw", default="0")
+    p.add_argument("--variants", default="0")
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--rule", default="ref")
     a = p.parse_args()
@@ -30,14 +31,16 @@ def main():
     h = a.size
     w = a.width or a.size
     variants = list(itertools.product([int(x) for x in a.depths.split(",")],
-                                      [int(x) for x in a.rpw.split(",")]))
+                                      [int(x) for x in a.rpw.split(",")],
+                                      [int(x) for x in a.variants.split(",")]))
     engines = {}
-    for d, r in variants:
-        e = pkg.Engine(h, w, rule=rule, device=0, tb_depth=d, rows_per_wave=r)
+    for d, r, kv in variants:
+        e = pkg.Engine(h, w, rule=rule, device=0, tb_depth=d, rows_per_wave=r,
+                       kernel_variant=kv)
         e.init_random(1)
         e.step(d)  # warm
         e.sync()
-        engines[(d, r)] = e
+        engines[(d, r, kv)] = e
         if len(engines) > 6:  # bound HBM use: 1 GiB per engine at 65536^2
             pass
     res = {v: [] for v in variants}
@@ -57,7 +60,7 @@ def main():
     for v in variants:
         r = sorted(res[v])
         med = r[len(r) // 2]
-        print(json.dumps({"tb_depth": v[0], "rows_per_wave": v[1] or "auto",
+        print(json.dumps({"tb_depth": v[0], "rows_per_wave": v[1] or "auto", "variant": v[2],
                           "gcups_wall_median": round(med[0], 1),
                           "gcups_wall_best": round(r[-1][0], 1),
                           "kernel_ms_avg": round(med[1], 4),

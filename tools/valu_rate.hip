@@ -1,0 +1,94 @@
+// valu_rate.hip -- dev microbenchmark: issue rate of the VALU instructions the
+// stencil uses (v_xor_b32 VOP2, v_bitop3_b32 / v_alignbit_b32 / v_xor3 VOP3,
+// v_mov_b32_dpp) on gfx950, to price the kernel against the VALU ceiling.
+// Each wave runs 16 independent accumulator chains; the grid fills every SIMD
+// with 4 waves.  Build: hipcc -O3 --offload-arch=gfx950 tools/valu_rate.hip -o /tmp/valu_rate
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHK(x)                                                                   \
+    do {                                                                         \
+        hipError_t e_ = (x);                                                     \
+        if (e_ != hipSuccess) {                                                  \
+            std::printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); \
+            std::exit(1);                                                        \
+        }                                                                        \
+    } while (0)
+
+constexpr int kIters = 4096;
+
+#define BODY16(INSTR)                                                                      \
+    asm volatile(INSTR(0) INSTR(1) INSTR(2) INSTR(3) INSTR(4) INSTR(5) INSTR(6) INSTR(7)  \
+                     INSTR(8) INSTR(9) INSTR(10) INSTR(11) INSTR(12) INSTR(13) INSTR(14)  \
+                     INSTR(15)                                                             \
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), \
+                   "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), \
+                   "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15])                      \
+                 : "v"(k1), "v"(k2))
+
+#define XOR(i) "v_xor_b32 %" #i ", %" #i ", %16\n"
+#define BITOP3(i) "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n"
+#define XOR3(i) "v_add3_u32 %" #i ", %" #i ", %16, %17\n"
+#define ALIGN(i) "v_alignbit_b32 %" #i ", %" #i ", %16, 31\n"
+#define DPP(i) "v_mov_b32_dpp %" #i ", %" #i " wave_shr:1 row_mask:0xf bank_mask:0xf\n"
+#define ANDOR(i) "v_and_or_b32 %" #i ", %" #i ", %16, %17\n"
+
+template <int OP>
+__global__ __launch_bounds__(256) void rate_kernel(unsigned* out, unsigned k1, unsigned k2)
+{
+    unsigned r[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = threadIdx.x * 16 + i;
+    for (int it = 0; it < kIters; ++it) {
+        if constexpr (OP == 0) BODY16(XOR);
+        if constexpr (OP == 1) BODY16(BITOP3);
+        if constexpr (OP == 2) BODY16(XOR3);
+        if constexpr (OP == 3) BODY16(ALIGN);
+        if constexpr (OP == 4) BODY16(DPP);
+        if constexpr (OP == 5) BODY16(ANDOR);
+    }
+    unsigned acc = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc ^= r[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+template <int OP>
+double run(unsigned* d, int blocks)
+{
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    hipLaunchKernelGGL(rate_kernel<OP>, dim3(blocks), dim3(256), 0, 0, d, 3u, 5u);  // warm
+    CHK(hipEventRecord(a));
+    for (int rep = 0; rep < 5; ++rep)
+        hipLaunchKernelGGL(rate_kernel<OP>, dim3(blocks), dim3(256), 0, 0, d, 3u, 5u);
+    CHK(hipEventRecord(b));
+    CHK(hipEventSynchronize(b));
+    float ms = 0;
+    CHK(hipEventElapsedTime(&ms, a, b));
+    const double waves = 5.0 * blocks * 4;
+    const double instr = waves * kIters * 16;  // wave-instructions
+    return instr / (ms * 1e-3);                // wave-instructions per second
+}
+
+int main()
+{
+    hipDeviceProp_t p;
+    CHK(hipGetDeviceProperties(&p, 0));
+    const int cus = p.multiProcessorCount;
+    const int blocks = cus * 4;  // 4 blocks x 4 waves per CU = 4 waves per SIMD
+    unsigned* d;
+    CHK(hipMalloc(&d, sizeof(unsigned) * blocks * 256));
+    const char* names[] = {"v_xor_b32", "v_bitop3_b32", "v_add3_u32", "v_alignbit_b32",
+                           "v_mov_b32_dpp", "v_and_or_b32"};
+    double r[6] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks),
+                   run<4>(d, blocks), run<5>(d, blocks)};
+    std::printf("{\"cus\": %d, \"clock_mhz_prop\": %d", cus, p.clockRate / 1000);
+    for (int i = 0; i < 6; ++i)
+        std::printf(", \"%s\": %.4g", names[i], r[i] / (4.0 * cus));  // per SIMD per second
+    std::printf(", \"unit\": \"wave-instructions per SIMD per second\"}\n");
+    return 0;
+}
