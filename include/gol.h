@@ -81,7 +81,7 @@ typedef struct gol_config {
 typedef struct gol_engine gol_engine;
 
 typedef struct gol_timing {
-    uint64_t launches;     /* stencil kernel launches timed */
+    uint64_t launches;     /* stencil kernel launches timed (sampled) */
     double kernel_ms;      /* sum of their HIP-event durations */
     double cell_gens;      /* cell-generations those launches produced (own rows) */
     double cell_gens_computed; /* including redundant halo/overlap work */
@@ -125,14 +125,19 @@ gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash);
 void gol_destroy(gol_engine* e);
 const char* gol_last_error(void);
 
-/* Per-launch HIP-event timing of the stencil kernel, on the engine's stream. */
-gol_status gol_set_timing(gol_engine* e, int enable);
+/* HIP-event timing of the stencil kernel on the engine's stream: events bracket
+ * every `every`-th launch (1 = all; 0 = off).  An event pair costs a few
+ * microseconds of stream time, so sample short launches (bench.py uses 8).
+ * gol_timing then covers the sampled launches only. */
+gol_status gol_set_timing(gol_engine* e, int every);
 gol_status gol_get_timing(gol_engine* e, gol_timing* out);
 gol_status gol_reset_timing(gol_engine* e);
 
-/* Engine geometry as chosen (for tools / tests). */
+/* Engine geometry as chosen (for tools / tests); any out pointer may be NULL.
+ * rows_per_wave: the rows each wavefront streams in a full-depth launch. */
 gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0,
-                    uint64_t* rows, uint32_t* tb_depth, uint32_t* halo_depth);
+                    uint64_t* rows, uint32_t* tb_depth, uint32_t* halo_depth,
+                    uint32_t* rows_per_wave);
 
 /* ---- Multi-GPU, one process per GPU (replaces the MPI stripes :70-81 and the
  * halo exchange :104-145 with RCCL send/recv over xGMI) ---- */

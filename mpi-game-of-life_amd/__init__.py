@@ -107,7 +107,8 @@ def lib():
     L.gol_set_timing.argtypes = [vp, i32]
     L.gol_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
     L.gol_reset_timing.argtypes = [vp]
-    L.gol_info.argtypes = [vp, pu64, pu64, pu64, pu64, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    L.gol_info.argtypes = [vp, pu64, pu64, pu64, pu64, ctypes.POINTER(u32), ctypes.POINTER(u32),
+                           ctypes.POINTER(u32)]
     L.gol_rank_rows.argtypes = [u64, i32, i32, pu64, pu64]
     L.gol_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.gol_create_group.argtypes = [u64, u64, ctypes.POINTER(Config), i32,
@@ -177,10 +178,12 @@ class Engine:
                                          ctypes.byref(handle)))
         self._h = handle
         h_, w_, r0, rows = (ctypes.c_uint64() for _ in range(4))
-        k, hx = ctypes.c_uint32(), ctypes.c_uint32()
+        k, hx, rpw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
         _check(lib().gol_info(self._h, ctypes.byref(h_), ctypes.byref(w_), ctypes.byref(r0),
-                              ctypes.byref(rows), ctypes.byref(k), ctypes.byref(hx)))
+                              ctypes.byref(rows), ctypes.byref(k), ctypes.byref(hx),
+                              ctypes.byref(rpw)))
         self.row0, self.rows, self.tb_depth, self.halo_depth = r0.value, rows.value, k.value, hx.value
+        self.rows_per_wave = rpw.value
 
     def close(self):
         if self._h:
@@ -234,8 +237,9 @@ class Engine:
         _check(lib().gol_digest(self._h, ctypes.byref(live), ctypes.byref(hsh)))
         return live.value, hsh.value
 
-    def set_timing(self, on=True):
-        _check(lib().gol_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, every=1):
+        """Time every `every`-th stencil launch with HIP events (0/False = off)."""
+        _check(lib().gol_set_timing(self._h, int(every)))
 
     def reset_timing(self):
         _check(lib().gol_reset_timing(self._h))

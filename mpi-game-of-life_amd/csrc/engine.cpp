@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/gol.h"
+#include "bitlayout.h"
 #include "life_internal.h"
 
 using gol::SegDesc;
@@ -87,7 +88,7 @@ bool pack_ascii(const char* buf, uint64_t rows, uint64_t w, uint64_t stride, uin
                     if (q < wq) {
                         const uint64_t c0 = q * 64, n = std::min<uint64_t>(64, w - c0);
                         for (uint64_t j = 0; j < n; ++j)
-                            v |= (uint64_t)(line[c0 + j] == '1') << j;
+                            v |= (uint64_t)(line[c0 + j] == '1') << gol_split_bit((unsigned)j);
                     }
                     out[q] = v;
                 }
@@ -111,7 +112,8 @@ void unpack_ascii(const uint64_t* src, uint64_t rows, uint64_t w, uint64_t strid
             for (uint64_t r = r0; r < r1; ++r) {
                 char* line = buf + r * (w + 1);
                 const uint64_t* in = src + r * stride;
-                for (uint64_t c = 0; c < w; ++c) line[c] = ((in[c >> 6] >> (c & 63)) & 1) ? '1' : '0';
+                for (uint64_t c = 0; c < w; ++c)
+                    line[c] = ((in[c >> 6] >> gol_split_bit((unsigned)(c & 63))) & 1) ? '1' : '0';
                 line[w] = '\n';
             }
         });
@@ -159,6 +161,7 @@ struct gol_engine {
     // plans: plan p = a device table of nseg SegDesc (+ host copy)
     struct Plan {
         std::vector<SegDesc> segs;
+        int64_t rpw = 0;  // rows per wavefront
         int64_t total_units = 0;
         SegDesc* dev = nullptr;
     };
@@ -170,8 +173,9 @@ struct gol_engine {
 
     unsigned long long* d_acc = nullptr;
 
-    // timing
-    bool timing = false;
+    // timing: HIP events around every `timing_every`-th stencil launch (0 = off)
+    uint32_t timing_every = 0;
+    uint64_t launch_count = 0;
     std::vector<hipEvent_t> ev_free;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
     std::vector<double> pending_cells, pending_cells_comp;
@@ -198,27 +202,52 @@ void finish_segs(std::vector<SegDesc>& segs, int64_t rpw, int32_t strips)
     }
 }
 
-gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
+// Rows per wavefront for one launch plan.  Every wavefront of a launch does the
+// same work, (R + K + 1) stage-steps of K stages (R output rows, K+1 rows of
+// warm-up/halo), so the launch time is set by the most loaded SIMD:
+// n = ceil(units / SIMDs) wavefronts run in rounds of `occ` resident ones, and
+// a partial round of m wavefronts still costs max(2, m) issue slots per
+// instruction (one wavefront alone issues at half the SIMD's VALU rate).
+// Measured (profiles/r01/sweep_rows_per_wave*.jsonl): keeping fewer than `occ`
+// wavefronts per SIMD all launch long is 5-10% slower than the model says, so
+// R is restricted to n >= occ whenever the field is large enough.
+int64_t pick_rows_per_wave(const std::vector<SegDesc>& segs, int32_t strips, int K, int occ,
+                           int simds)
 {
-    // choose rows per wavefront: enough wavefronts to fill 256 CUs several times
-    int64_t rpw = e->rows_per_wave;
-    if (rpw == 0) {
-        // 128 rows measured best at 65536^2, K = 8 (profiles/); halve while the
-        // launch has fewer than ~2 wavefronts per SIMD (256 CUs x 4 SIMDs)
-        rpw = 128;
-        const int64_t min_rpw = std::max<int64_t>(16, 2 * e->K);
-        while (rpw > min_rpw) {
-            std::vector<SegDesc> t = raw[0];
-            finish_segs(t, rpw, e->strips);
-            if (plan_units(t, e->strips) >= 2048) break;
-            rpw /= 2;
+    const int64_t c0 = 3;  // per-wavefront fixed cost, in rows
+    int64_t maxrows = 1;
+    for (const auto& s : segs) maxrows = std::max<int64_t>(maxrows, s.out_hi - s.out_lo);
+    int64_t best_r[2] = {16, 16};
+    double best[2] = {1e300, 1e300};
+    for (int64_t R = std::max<int64_t>(8, K + 2); R <= std::min<int64_t>(1024, maxrows + K); ++R) {
+        std::vector<SegDesc> t = segs;
+        finish_segs(t, R, strips);
+        const int64_t units = plan_units(t, strips);
+        const int64_t n = (units + simds - 1) / simds;
+        const int64_t full = n / occ, rem = n % occ;
+        const double slots =
+            (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
+        const double cost = slots * (double)(R + K + 1 + c0);
+        const int filled = n >= occ ? 1 : 0;
+        if (cost < best[filled] * 0.999) {
+            best[filled] = cost;
+            best_r[filled] = R;
         }
     }
-    e->rows_per_wave = (uint32_t)rpw;
+    return best[1] < 1e300 ? best_r[1] : best_r[0];
+}
+
+gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
+{
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
+    const int occ = std::max(1, gol::life_blocks_per_cu((int)e->K, e->rule, e->compact));
     for (const auto& r : raw) {
         gol_engine::Plan p;
         p.segs = r;
-        finish_segs(p.segs, rpw, e->strips);
+        p.rpw = e->rows_per_wave ? (int64_t)e->rows_per_wave
+                                 : pick_rows_per_wave(r, e->strips, (int)e->K, occ, 4 * cus);
+        finish_segs(p.segs, p.rpw, e->strips);
         p.total_units = plan_units(p.segs, e->strips);
         HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * p.segs.size()));
         HIP_TRY(hipMemcpy(p.dev, p.segs.data(), sizeof(SegDesc) * p.segs.size(),
@@ -381,20 +410,21 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth)
     a.strips = e->strips;
     a.stride = (int64_t)e->stride;
     a.wq = (int64_t)e->wq;
-    a.lastmask = e->lastmask;
-    a.rows_per_wave = e->rows_per_wave;
+    a.lastmask = gol_split64(e->lastmask);  // the kernel works on column-split words
+    a.rows_per_wave = p.rpw;
     a.total_units = p.total_units;
     a.birth = e->birth;
     a.survive = e->survive;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (e->timing) {
+    const bool timed = e->timing_every && (e->launch_count++ % e->timing_every) == 0;
+    if (timed) {
         gol_status st = get_event(e, &e0);
         if (st == GOL_OK) st = get_event(e, &e1);
         if (st != GOL_OK) return st;
         HIP_TRY(hipEventRecord(e0, e->stream));
     }
     HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->compact, e->stream));
-    if (e->timing) {
+    if (timed) {
         HIP_TRY(hipEventRecord(e1, e->stream));
         e->ev_pending.push_back({e0, e1});
         double own = 0, comp = 0;
@@ -640,10 +670,13 @@ static uint64_t load_rows_needed(const gol_engine* e)
     return e->nranks > 1 ? e->R : e->H;
 }
 
-gol_status gol_load_packed(gol_engine* e, const uint64_t* words, uint64_t rs)
+}  // extern "C"
+
+// Host <-> device transfer of the load/store regions.  `canonical` words use the
+// public bit order (bit j = column 64q+j) and are converted to/from the
+// engine's column-split words (bitlayout.h); otherwise words are already split.
+static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs, bool canonical)
 {
-    if (!e || !words) return fail(GOL_EINVAL, "null argument");
-    if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
     HIP_TRY(hipSetDevice(e->device));
     // clear everything (halos, unused rows) then copy each region, masking pad bits
     const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
@@ -655,14 +688,47 @@ gol_status gol_load_packed(gol_engine* e, const uint64_t* words, uint64_t rs)
         for (uint64_t i = 0; i < r.rows; ++i) {
             const uint64_t* src = words + (urow + i) * rs;
             uint64_t* dst = tmp.data() + i * e->stride;
-            for (uint64_t q = 0; q < e->wq; ++q) dst[q] = src[q];
-            dst[e->wq - 1] &= e->lastmask;
+            if (canonical) {
+                for (uint64_t q = 0; q < e->wq; ++q)
+                    dst[q] = gol_split64(q == e->wq - 1 ? (src[q] & e->lastmask) : src[q]);
+            } else {
+                for (uint64_t q = 0; q < e->wq; ++q) dst[q] = src[q];
+                dst[e->wq - 1] &= gol_split64(e->lastmask);
+            }
         }
         HIP_TRY(hipMemcpyAsync(e->buf[e->cur] + r.buf_row * e->stride, tmp.data(),
                                tmp.size() * 8, hipMemcpyHostToDevice, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
     }
     return GOL_OK;
+}
+
+static gol_status download(gol_engine* e, uint64_t* words, uint64_t rs, bool canonical)
+{
+    HIP_TRY(hipSetDevice(e->device));
+    std::vector<uint64_t> tmp;
+    for (const auto& r : e->user_regions) {
+        tmp.resize((size_t)r.rows * e->stride);
+        HIP_TRY(hipMemcpyAsync(tmp.data(), e->buf[e->cur] + r.buf_row * e->stride,
+                               tmp.size() * 8, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        const uint64_t urow = e->nranks > 1 ? 0 : r.user_row;
+        for (uint64_t i = 0; i < r.rows; ++i) {
+            uint64_t* dst = words + (urow + i) * rs;
+            const uint64_t* src = tmp.data() + i * e->stride;
+            for (uint64_t q = 0; q < e->wq; ++q) dst[q] = canonical ? gol_join64(src[q]) : src[q];
+        }
+    }
+    return GOL_OK;
+}
+
+extern "C" {
+
+gol_status gol_load_packed(gol_engine* e, const uint64_t* words, uint64_t rs)
+{
+    if (!e || !words) return fail(GOL_EINVAL, "null argument");
+    if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
+    return upload(e, words, rs, true);
 }
 
 gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
@@ -676,25 +742,14 @@ gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
     std::vector<uint64_t> packed((size_t)rows * e->stride);
     if (!pack_ascii(buf, rows, e->W, e->stride, packed.data()))
         return fail(GOL_EINVAL, "malformed ASCII: a line is not w cells followed by '\\n'");
-    return gol_load_packed(e, packed.data(), e->stride);
+    return upload(e, packed.data(), e->stride, false);
 }
 
 gol_status gol_store_packed(gol_engine* e, uint64_t* words, uint64_t rs)
 {
     if (!e || !words) return fail(GOL_EINVAL, "null argument");
     if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
-    HIP_TRY(hipSetDevice(e->device));
-    std::vector<uint64_t> tmp;
-    for (const auto& r : e->user_regions) {
-        tmp.resize((size_t)r.rows * e->stride);
-        HIP_TRY(hipMemcpyAsync(tmp.data(), e->buf[e->cur] + r.buf_row * e->stride,
-                               tmp.size() * 8, hipMemcpyDeviceToHost, e->stream));
-        HIP_TRY(hipStreamSynchronize(e->stream));
-        const uint64_t urow = e->nranks > 1 ? 0 : r.user_row;
-        for (uint64_t i = 0; i < r.rows; ++i)
-            std::memcpy(words + (urow + i) * rs, tmp.data() + i * e->stride, e->wq * 8);
-    }
-    return GOL_OK;
+    return download(e, words, rs, true);
 }
 
 gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
@@ -705,7 +760,7 @@ gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
         return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
                                     std::to_string(rows * (e->W + 1)));
     std::vector<uint64_t> packed((size_t)rows * e->stride);
-    gol_status st = gol_store_packed(e, packed.data(), e->stride);
+    gol_status st = download(e, packed.data(), e->stride, false);
     if (st != GOL_OK) return st;
     unpack_ascii(packed.data(), rows, e->W, e->stride, buf);
     return GOL_OK;
@@ -860,10 +915,12 @@ gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
     return GOL_OK;
 }
 
-gol_status gol_set_timing(gol_engine* e, int enable)
+gol_status gol_set_timing(gol_engine* e, int every)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
-    e->timing = enable != 0;
+    if (every < 0) return fail(GOL_EINVAL, "timing sample interval must be >= 0");
+    e->timing_every = (uint32_t)every;
+    e->launch_count = 0;
     return GOL_OK;
 }
 
@@ -886,8 +943,9 @@ gol_status gol_reset_timing(gol_engine* e)
 }
 
 gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uint64_t* rows,
-                    uint32_t* tb_depth, uint32_t* halo_depth)
+                    uint32_t* tb_depth, uint32_t* halo_depth, uint32_t* rows_per_wave)
 {
+    if (e && rows_per_wave) *rows_per_wave = e->plans.empty() ? 0 : (uint32_t)e->plans.back().rpw;
     if (!e) return fail(GOL_EINVAL, "null engine");
     if (h) *h = e->H;
     if (w) *w = e->W;

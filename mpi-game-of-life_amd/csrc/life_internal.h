@@ -59,6 +59,10 @@ constexpr int kDepthList[] = {16, 12, 8, 7, 6, 4, 2, 1};
 // 10-dword stage state (more waves per SIMD, 4 more VALU ops per word-generation).
 hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, bool compact, hipStream_t s);
 
+// Resident 256-thread blocks per CU of the stencil kernel for (depth, rule,
+// variant) -- each block is one wavefront per SIMD (occupancy query).
+int life_blocks_per_cu(int depth, RuleKind rule, bool compact);
+
 // Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field
 // rows [glob_row0, glob_row0+nrows).
 hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_t lastmask,

@@ -8,9 +8,11 @@
 // Kernel shape (one wavefront = one work unit, no LDS, no barriers):
 //   * A wavefront owns a strip of 64 consecutive words of a row (lane l holds
 //     word strip*62 - 1 + l); lanes 0 and 63 are the horizontal halo, so each
-//     strip outputs 62 words.  Horizontal neighbour bits come from the adjacent
-//     lanes by DPP wave shifts (wave_shr:1 / wave_shl:1) and v_alignbit funnel
-//     shifts.  After g fused generations the contamination from the unknown
+//     strip outputs 62 words.  Words are column-split (bitlayout.h: even columns
+//     in the low dword, odd in the high), so two of the four horizontal
+//     neighbour planes are free; the other two are one v_alignbit each, with the
+//     carry bit from the adjacent lane by a DPP wave shift (wave_shr:1 /
+//     wave_shl:1).  After g fused generations the contamination from the unknown
 //     words beyond the halo lanes has moved g bits into lanes 0/63, so K <= 63
 //     keeps lanes 1..62 exact.
 //   * The wavefront streams down `rows_per_wave` output rows of its strip, K rows
@@ -27,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bitlayout.h"
 #include "life_internal.h"
 
 namespace gol {
@@ -107,26 +110,38 @@ __device__ __forceinline__ uint32_t rule32(uint32_t as, uint32_t ac, uint32_t bs
     }
 }
 
+// Horizontal neighbour planes of a column-split word x (bitlayout.h): lo = even
+// columns, hi = odd columns.  An even column's right neighbour and an odd
+// column's left neighbour are the other half at the same bit; the remaining two
+// planes take one funnel shift each, with the carry bit from the adjacent lane.
+struct Horiz {
+    uint32_t Le, Ro;  // left of the even columns, right of the odd columns
+};
+__device__ __forceinline__ Horiz horiz(u2 x)
+{
+    const uint32_t hp = lane_from_left(x.hi);   // odd columns of word q-1 (bit 31: col 64q-1)
+    const uint32_t ln = lane_from_right(x.lo);  // even columns of word q+1 (bit 0: col 64q+64)
+    Horiz h;
+    h.Le = __builtin_amdgcn_alignbit(x.hi, hp, 31);  // (hi << 1) | (hp >> 31)
+    h.Ro = __builtin_amdgcn_alignbit(ln, x.lo, 1);   // (lo >> 1) | (ln << 31)
+    return h;
+}
+
 // One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
 template <int RULE>
 __device__ __forceinline__ u2 stage_step(Stage& st, u2 x, uint32_t birth, uint32_t survive)
 {
-    const uint32_t lh = lane_from_left(x.hi);   // hi half of word q-1
-    const uint32_t rl = lane_from_right(x.lo);  // lo half of word q+1
-    // L: neighbour at column c-1 (bit j <- bit j-1); R: column c+1 (bit j <- bit j+1)
-    const uint32_t Llo = __builtin_amdgcn_alignbit(x.lo, lh, 31);
-    const uint32_t Lhi = __builtin_amdgcn_alignbit(x.hi, x.lo, 31);
-    const uint32_t Rlo = __builtin_amdgcn_alignbit(x.hi, x.lo, 1);
-    const uint32_t Rhi = __builtin_amdgcn_alignbit(rl, x.hi, 1);
+    const Horiz hz = horiz(x);
+    // even half: (L, C, R) = (Le, lo, hi); odd half: (lo, hi, Ro)
     u2 s2, c2, s3, c3;
-    s2.lo = Llo ^ Rlo;
-    s2.hi = Lhi ^ Rhi;
-    c2.lo = Llo & Rlo;
-    c2.hi = Lhi & Rhi;
-    s3.lo = lop3<kXor3>(Llo, x.lo, Rlo);
-    s3.hi = lop3<kXor3>(Lhi, x.hi, Rhi);
-    c3.lo = lop3<kMaj>(Llo, x.lo, Rlo);
-    c3.hi = lop3<kMaj>(Lhi, x.hi, Rhi);
+    s2.lo = hz.Le ^ x.hi;
+    c2.lo = hz.Le & x.hi;
+    s3.lo = lop3<kXor3>(hz.Le, x.lo, x.hi);
+    c3.lo = lop3<kMaj>(hz.Le, x.lo, x.hi);
+    s2.hi = x.lo ^ hz.Ro;
+    c2.hi = x.lo & hz.Ro;
+    s3.hi = lop3<kXor3>(x.lo, x.hi, hz.Ro);
+    c3.hi = lop3<kMaj>(x.lo, x.hi, hz.Ro);
     u2 y;
     y.lo = rule32<RULE>(st.ps.lo, st.pc.lo, st.hs.lo, st.hc.lo, s3.lo, c3.lo, st.al.lo, birth,
                         survive);
@@ -156,25 +171,20 @@ constexpr uint32_t kOrAnd = 0xF8;  // a | (b & c)
 template <int RULE>
 __device__ __forceinline__ u2 stage_step(StageC& st, u2 x, uint32_t birth, uint32_t survive)
 {
-    const uint32_t lh = lane_from_left(x.hi);
-    const uint32_t rl = lane_from_right(x.lo);
-    const uint32_t Llo = __builtin_amdgcn_alignbit(x.lo, lh, 31);
-    const uint32_t Lhi = __builtin_amdgcn_alignbit(x.hi, x.lo, 31);
-    const uint32_t Rlo = __builtin_amdgcn_alignbit(x.hi, x.lo, 1);
-    const uint32_t Rhi = __builtin_amdgcn_alignbit(rl, x.hi, 1);
+    const Horiz hz = horiz(x);
     u2 y;
-    y.lo = rule32<RULE>(st.ps.lo, st.pc.lo, st.hs.lo, st.hc.lo, lop3<kXor3>(Llo, x.lo, Rlo),
-                        lop3<kMaj>(Llo, x.lo, Rlo), st.al.lo, birth, survive);
-    y.hi = rule32<RULE>(st.ps.hi, st.pc.hi, st.hs.hi, st.hc.hi, lop3<kXor3>(Lhi, x.hi, Rhi),
-                        lop3<kMaj>(Lhi, x.hi, Rhi), st.al.hi, birth, survive);
+    y.lo = rule32<RULE>(st.ps.lo, st.pc.lo, st.hs.lo, st.hc.lo, lop3<kXor3>(hz.Le, x.lo, x.hi),
+                        lop3<kMaj>(hz.Le, x.lo, x.hi), st.al.lo, birth, survive);
+    y.hi = rule32<RULE>(st.ps.hi, st.pc.hi, st.hs.hi, st.hc.hi, lop3<kXor3>(x.lo, x.hi, hz.Ro),
+                        lop3<kMaj>(x.lo, x.hi, hz.Ro), st.al.hi, birth, survive);
     st.ps.lo = st.hs.lo ^ st.al.lo;
     st.ps.hi = st.hs.hi ^ st.al.hi;
     st.pc.lo = lop3<kOrAnd>(st.hc.lo, st.hs.lo, st.al.lo);
     st.pc.hi = lop3<kOrAnd>(st.hc.hi, st.hs.hi, st.al.hi);
-    st.hs.lo = Llo ^ Rlo;
-    st.hs.hi = Lhi ^ Rhi;
-    st.hc.lo = Llo & Rlo;
-    st.hc.hi = Lhi & Rhi;
+    st.hs.lo = hz.Le ^ x.hi;
+    st.hs.hi = x.lo ^ hz.Ro;
+    st.hc.lo = hz.Le & x.hi;
+    st.hc.hi = x.lo & hz.Ro;
     st.al = x;
     return y;
 }
@@ -315,6 +325,30 @@ hipError_t launch_variant(const StepArgs& a, RuleKind rule, bool compact, hipStr
     return compact ? launch_depth<K, true>(a, rule, s) : launch_depth<K, false>(a, rule, s);
 }
 
+template <int K, bool COMPACT>
+int occupancy_of(RuleKind rule)
+{
+    int blocks = 0;
+    hipError_t e = hipErrorInvalidValue;
+    const int threads = 64 * kWavesPerBlock;
+    if (rule == RULE_REF)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, life_tb_kernel<K, RULE_REF, COMPACT>, threads, 0);
+    else if (rule == RULE_CONWAY)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, life_tb_kernel<K, RULE_CONWAY, COMPACT>, threads, 0);
+    else
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, life_tb_kernel<K, RULE_GENERIC, COMPACT>, threads, 0);
+    return e == hipSuccess ? blocks : 0;
+}
+
+template <int K>
+int occupancy_variant(RuleKind rule, bool compact)
+{
+    return compact ? occupancy_of<K, true>(rule) : occupancy_of<K, false>(rule);
+}
+
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t idx)
 {
     uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
@@ -335,9 +369,9 @@ __global__ __launch_bounds__(256) void init_random_kernel(uint64_t* buf, int64_t
         uint64_t v = 0;
         if (q < wq) {
             v = splitmix64_at(seed, (uint64_t)(glob_row0 + i) * (uint64_t)wq + (uint64_t)q);
-            if (q == wq - 1) v &= lastmask;
+            if (q == wq - 1) v &= lastmask;  // canonical mask
         }
-        buf[(row_base + i) * stride + q] = v;
+        buf[(row_base + i) * stride + q] = gol_split64(v);
     }
 }
 
@@ -351,7 +385,7 @@ __global__ __launch_bounds__(256) void digest_kernel(const uint64_t* buf, int64_
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = k / wq, q = k - i * wq;
-        const uint64_t v = buf[(row_base + i) * stride + q];
+        const uint64_t v = gol_join64(buf[(row_base + i) * stride + q]);
         live += (uint64_t)__popcll(v);
         const uint64_t idx = (uint64_t)(glob_row0 + i) * (uint64_t)wq + (uint64_t)q;
         hash += splitmix64_at(v ^ splitmix64_at(0, idx), 0);
@@ -381,6 +415,21 @@ hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, bool compact
     case 12: return launch_variant<12>(a, rule, compact, s);
     case 16: return launch_variant<16>(a, rule, compact, s);
     default: return hipErrorInvalidValue;
+    }
+}
+
+int life_blocks_per_cu(int depth, RuleKind rule, bool compact)
+{
+    switch (depth) {
+    case 1: return occupancy_variant<1>(rule, compact);
+    case 2: return occupancy_variant<2>(rule, compact);
+    case 4: return occupancy_variant<4>(rule, compact);
+    case 6: return occupancy_variant<6>(rule, compact);
+    case 7: return occupancy_variant<7>(rule, compact);
+    case 8: return occupancy_variant<8>(rule, compact);
+    case 12: return occupancy_variant<12>(rule, compact);
+    case 16: return occupancy_variant<16>(rule, compact);
+    default: return 0;
     }
 }
 

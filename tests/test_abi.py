@@ -84,3 +84,20 @@ def test_c_abi_from_c(pkg, tmp_path):
                     f"-Wl,-rpath,{os.path.dirname(pkg.LIB_PATH)}"], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
     assert out.split() == ["34", "33", "4"]
+
+
+def test_column_split_layout(tmp_path):
+    """bitlayout.h: split/join are inverse permutations and gol_split_bit agrees."""
+    src = tmp_path / "t.cpp"
+    src.write_text(
+        '#include "bitlayout.h"\n#include <cstdio>\n#include <random>\n'
+        "int main(){std::mt19937_64 r(1);\n"
+        " for(int i=0;i<100000;++i){uint64_t c=r(); uint64_t v=gol_split64(c);\n"
+        "  if(gol_join64(v)!=c) return 1;\n"
+        "  for(unsigned j=0;j<64;++j) if(((c>>j)&1)!=((v>>gol_split_bit(j))&1)) return 2;}\n"
+        " if(gol_split64(1ull)!=1ull || gol_split64(2ull)!=(1ull<<32)) return 3;\n"
+        " std::puts(\"ok\"); return 0;}\n")
+    exe = tmp_path / "t"
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-I{ROOT}/mpi-game-of-life_amd/csrc", str(src),
+                    "-o", str(exe)], check=True)
+    assert subprocess.run([str(exe)], capture_output=True, text=True).stdout.strip() == "ok"

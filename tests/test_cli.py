@@ -5,7 +5,6 @@ import hashlib
 import json
 import os
 import re
-import shutil
 import subprocess
 
 import pytest
@@ -16,9 +15,9 @@ GOLD = json.load(open(os.path.join(GOLDEN, "ref_outputs.json")))
 
 
 def setup_dir(tmp_path, epochs, h=1500, w=500, data=None):
-    shutil.copy(os.path.join(GOLDEN, "data.txt"), tmp_path / "data.txt")
-    if data is not None:
-        (tmp_path / "data.txt").write_bytes(data)
+    if data is None:
+        data = open(os.path.join(GOLDEN, "data.txt"), "rb").read()
+    (tmp_path / "data.txt").write_bytes(data)
     (tmp_path / "grid_size_data.txt").write_text(f"{h} {w} {epochs}")
     return tmp_path
 

@@ -22,9 +22,11 @@ def test_group_matches_single_field(pkg, oracle, nranks, rule):
     R = {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}[rule]
     h, w = 203, 4000
     g = oracle.bp_random(h, w, 3 + nranks)
-    for tb, hx, gens in ((8, 0, 37), (4, 12, 30), (2, 5, 11), (1, 3, 7), (16, 16, 33)):
+    for tb, hx, gens, kv in ((8, 0, 37, 1), (4, 12, 30, 1), (2, 5, 11, 1), (1, 3, 7, 1),
+                             (16, 16, 33, 1), (8, 0, 37, 2), (16, 24, 50, 2)):
         ref = oracle.bp_run(g, w, gens, R)
-        with pkg.Group(h, w, nranks, rule=R, tb_depth=tb, halo_depth=hx) as grp:
+        with pkg.Group(h, w, nranks, rule=R, tb_depth=tb, halo_depth=hx,
+                       kernel_variant=kv) as grp:
             grp.load_packed(g)
             grp.step(gens)
             grp.sync()

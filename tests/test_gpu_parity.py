@@ -87,12 +87,14 @@ def test_random_fields_every_depth(pkg, oracle, shape, rule):
 
 
 @pytest.mark.parametrize("rpw", [16, 32, 48, 100])
-def test_row_blocking(pkg, oracle, rpw):
+@pytest.mark.parametrize("variant", [1, 2])
+def test_row_blocking(pkg, oracle, rpw, variant):
     """Many row blocks per strip (rows_per_wave small): block seams exact."""
     h, w = 300, 4100
     g = oracle.bp_random(h, w, 5)
     ref = oracle.bp_run(g, w, 16, oracle.CONWAY)
-    with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw) as e:
+    with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw,
+                    kernel_variant=variant) as e:
         e.init_random(5)
         e.step(16)
         assert (e.store_packed() == ref).all()
@@ -203,3 +205,13 @@ def test_timing_counters(pkg):
     assert t["launches"] == 3
     assert t["kernel_ms"] > 0
     assert t["cell_gens"] == 1024 * 1024 * 20
+
+
+def test_timing_sampled(pkg):
+    with pkg.Engine(1024, 1024, device=0, tb_depth=8) as e:
+        e.init_random(1)
+        e.set_timing(2)
+        e.step(40)  # 5 launches of 8; launches 0, 2, 4 are timed
+        t = e.timing()
+    assert t["launches"] == 3
+    assert t["cell_gens"] == 1024 * 1024 * 24

@@ -25,6 +25,7 @@ def main():
     p.add_argument("--variants", default="0")
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--rule", default="ref")
+    p.add_argument("--no-events", action="store_true", help="time wall clock only")
     a = p.parse_args()
     pkg = entry.load_package()
     rule = pkg.REF_RULE if a.rule == "ref" else pkg.CONWAY
@@ -47,7 +48,7 @@ def main():
     for _ in range(a.rounds):
         for v in variants:
             e = engines[v]
-            e.set_timing(True)
+            e.set_timing(0 if a.no_events else 8)
             e.reset_timing()
             t0 = time.perf_counter()
             e.step(a.gens)
@@ -60,7 +61,8 @@ def main():
     for v in variants:
         r = sorted(res[v])
         med = r[len(r) // 2]
-        print(json.dumps({"tb_depth": v[0], "rows_per_wave": v[1] or "auto", "variant": v[2],
+        print(json.dumps({"tb_depth": v[0], "rows_per_wave": v[1] or f"auto({engines[v].rows_per_wave})",
+                          "variant": v[2],
                           "gcups_wall_median": round(med[0], 1),
                           "gcups_wall_best": round(r[-1][0], 1),
                           "kernel_ms_avg": round(med[1], 4),
