@@ -12,6 +12,9 @@
 // --ref-ranks P reproduces `mpirun -np P` byte for byte (GOL_SEM_REF_STRIPES:
 // the reference's halo exchange is a no-op, so its output depends on P).
 // Without it the field evolves as one domain (== the reference at -np 1).
+// --gpus G splits that domain into G row stripes on devices 0..G-1 of this
+// process with k-deep halo rounds over xGMI peer copies (gol_create_group);
+// --stripes S runs S stripes round-robin on the G devices (S >= G).
 //
 // Deviation: where the reference prints an error and continues with
 // uninitialised values (:206) or an unopened file (:186), this program exits
@@ -68,6 +71,7 @@ void usage()
 {
     std::cerr << "usage: gol [--dir DIR] [--ref-ranks P] [--rule ref|conway|B3/S23]\n"
                  "           [--tb-depth K] [--rows-per-wave N] [--device D]\n"
+                 "           [--gpus G] [--stripes S] [--halo-depth H]\n"
                  "Reads grid_size_data.txt and data.txt, writes output.txt.\n";
 }
 
@@ -92,6 +96,7 @@ int main(int argc, char** argv)
 {
     const auto t0 = std::chrono::steady_clock::now();  // MPI_Wtime() at :199
     std::string dir = ".";
+    int gpus = 0, stripes = 0;
     gol_config cfg;
     gol_config_init(&cfg);
     for (int i = 1; i < argc; ++i) {
@@ -115,6 +120,9 @@ int main(int argc, char** argv)
         } else if (a == "--tb-depth") cfg.tb_depth = (uint32_t)std::strtoul(next().c_str(), nullptr, 10);
         else if (a == "--rows-per-wave") cfg.rows_per_wave = (uint32_t)std::strtoul(next().c_str(), nullptr, 10);
         else if (a == "--device") cfg.device = (int32_t)std::strtol(next().c_str(), nullptr, 10);
+        else if (a == "--gpus") gpus = (int)std::strtol(next().c_str(), nullptr, 10);
+        else if (a == "--stripes") stripes = (int)std::strtol(next().c_str(), nullptr, 10);
+        else if (a == "--halo-depth") cfg.halo_depth = (uint32_t)std::strtoul(next().c_str(), nullptr, 10);
         else if (a == "-h" || a == "--help") {
             usage();
             return 0;
@@ -149,9 +157,43 @@ int main(int argc, char** argv)
     }
 
     std::vector<char> out(bytes);
+    if (gpus > 0 || stripes > 0) {
+        if (cfg.semantics != GOL_SEM_GLOBAL) {
+            std::cerr << "--gpus/--stripes evolve one global field; drop --ref-ranks" << std::endl;
+            return 1;
+        }
+        if (gpus <= 0) gpus = 1;
+        if (stripes <= 0) stripes = gpus;
+        if ((uint64_t)h / (uint64_t)stripes == 0) {
+            std::cerr << "Need 1 <= stripes <= rows." << std::endl;
+            return 1;
+        }
+    }
     if (epochs == 0) {
         // zero generations: the reference writes the input bytes back (:157-164)
         out = data;
+    } else if (stripes > 0) {
+        std::vector<gol_engine*> es((size_t)stripes, nullptr);
+        std::vector<int> devs((size_t)stripes);
+        for (int r = 0; r < stripes; ++r) devs[(size_t)r] = r % gpus;
+        gol_status st = gol_create_group((uint64_t)h, (uint64_t)w, &cfg, stripes, devs.data(),
+                                         es.data());
+        for (int r = 0; r < stripes && st == GOL_OK; ++r) {
+            uint64_t r0 = 0, n = 0;
+            gol_rank_rows((uint64_t)h, stripes, r, &r0, &n);
+            st = gol_load_ascii(es[(size_t)r], data.data() + r0 * (uint64_t)(w + 1),
+                                n * (uint64_t)(w + 1));
+        }
+        if (st == GOL_OK) st = gol_group_step(es.data(), stripes, (uint64_t)epochs);
+        for (int r = 0; r < stripes && st == GOL_OK; ++r) {
+            uint64_t r0 = 0, n = 0;
+            gol_rank_rows((uint64_t)h, stripes, r, &r0, &n);
+            st = gol_store_ascii(es[(size_t)r], out.data() + r0 * (uint64_t)(w + 1),
+                                 n * (uint64_t)(w + 1));
+        }
+        if (st != GOL_OK) std::cerr << "gol error " << (int)st << ": " << gol_last_error() << std::endl;
+        for (auto* e : es) gol_destroy(e);
+        if (st != GOL_OK) return 1;
     } else {
         gol_engine* e = nullptr;
         gol_status st = gol_create((uint64_t)h, (uint64_t)w, &cfg, &e);

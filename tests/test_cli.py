@@ -79,3 +79,15 @@ def test_cli_conway_rule(pkg, oracle, tmp_path):
     assert r.returncode == 0, r.stderr
     assert (d / "output.txt").read_bytes() == oracle.bp_unpack(
         oracle.bp_run(g, w, 9, oracle.CONWAY), w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stripes", [2, 5])
+def test_cli_stripes_intended_semantics(pkg, tmp_path, stripes):
+    """--stripes S (S row stripes with real halo exchange, one process) gives the
+    reference's intended result, i.e. its -np 1 output, for any S."""
+    case = [c for c in GOLD["cases"] if c["np"] == 1 and c["gens"] == 100][0]
+    d = setup_dir(tmp_path, 100)
+    r = run_cli(pkg, d, "--gpus", "1", "--stripes", str(stripes))
+    assert r.returncode == 0, r.stderr
+    assert hashlib.sha256((d / "output.txt").read_bytes()).hexdigest() == case["sha256"]
