@@ -153,6 +153,16 @@ struct gol_engine {
     bool grouped = false;
     hipEvent_t ev_ready = nullptr, ev_copied = nullptr;
 
+    // exchange/compute overlap (multi-rank): the last launch of a full round is
+    // split into a band launch (the rows the neighbours need) and an interior
+    // launch; the exchange runs on `comm` between them.  plans[Hx] = band,
+    // plans[Hx+1] = interior.  halo_fresh: the current buffer's halo rows were
+    // already exchanged (completion signalled by ev_xdone on `comm`).
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_band = nullptr, ev_xdone = nullptr;
+    bool overlap = false;
+    bool halo_fresh = false;
+
     uint64_t buf_rows = 0;
     uint64_t* alloc[2] = {nullptr, nullptr};
     uint64_t* buf[2] = {nullptr, nullptr};
@@ -161,7 +171,8 @@ struct gol_engine {
     // plans: plan p = a device table of nseg SegDesc (+ host copy)
     struct Plan {
         std::vector<SegDesc> segs;
-        int64_t rpw = 0;  // rows per wavefront
+        double own_rows = 0;  // output rows of this plan that are the caller's rows
+        int64_t rpw = 0;      // rows per wavefront
         int64_t total_units = 0;
         SegDesc* dev = nullptr;
     };
@@ -249,6 +260,23 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                                  : pick_rows_per_wave(r, e->strips, (int)e->K, occ, 4 * cus);
         finish_segs(p.segs, p.rpw, e->strips);
         p.total_units = plan_units(p.segs, e->strips);
+        for (const auto& sg : p.segs) {
+            // own rows of a segment: rank engines [Hx, Hx+R); REF_STRIPES the
+            // rank's output rows; GLOBAL all rows
+            int64_t olo = sg.out_lo, ohi = sg.out_hi;
+            if (e->nranks > 1) {
+                olo = std::max<int64_t>(olo, (int64_t)e->Hx);
+                ohi = std::min<int64_t>(ohi, (int64_t)(e->Hx + e->R));
+            } else if (e->sem == GOL_SEM_REF_STRIPES) {
+                for (const auto& ur : e->user_regions)
+                    if ((int64_t)ur.buf_row >= sg.base_row &&
+                        (int64_t)ur.buf_row < sg.base_row + sg.in_rows) {
+                        olo = std::max<int64_t>(olo, (int64_t)ur.buf_row - sg.base_row);
+                        ohi = std::min<int64_t>(ohi, (int64_t)(ur.buf_row + ur.rows) - sg.base_row);
+                    }
+            }
+            p.own_rows += (double)std::max<int64_t>(0, ohi - olo);
+        }
         HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * p.segs.size()));
         HIP_TRY(hipMemcpy(p.dev, p.segs.data(), sizeof(SegDesc) * p.segs.size(),
                           hipMemcpyHostToDevice));
@@ -295,6 +323,11 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
     if (cfg->device >= 0) HIP_TRY(hipSetDevice(cfg->device));
     HIP_TRY(hipGetDevice(&e->device));
     HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    if (e->nranks > 1) {
+        HIP_TRY(hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_band, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_xdone, hipEventDisableTiming));
+    }
 
     std::vector<std::vector<SegDesc>> raw;
     if (e->nranks > 1) {
@@ -313,6 +346,35 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
             s.out_lo = std::max<int64_t>((int64_t)c, in_field_lo);
             s.out_hi = std::min<int64_t>((int64_t)(e->buf_rows - c), in_field_hi);
             raw.push_back({s});
+        }
+        // overlap plans: rows neighbours need = own rows [Hx, 2Hx) (to rank-1) and
+        // [R, R+Hx) (to rank+1); interior = the rest of the own rows
+        const int64_t Hx = (int64_t)e->Hx, R = (int64_t)e->R;
+        if (R >= 2 * Hx) {
+            SegDesc b = raw.back()[0];  // shrink Hx: out = own rows
+            std::vector<SegDesc> band, inner;
+            int64_t ilo = Hx, ihi = Hx + R;
+            if (e->rank > 0) {
+                SegDesc t = b;
+                t.out_lo = Hx;
+                t.out_hi = 2 * Hx;
+                band.push_back(t);
+                ilo = 2 * Hx;
+            }
+            if (e->rank < e->nranks - 1) {
+                SegDesc t = b;
+                t.out_lo = R;
+                t.out_hi = R + Hx;
+                band.push_back(t);
+                ihi = R;
+            }
+            SegDesc t = b;
+            t.out_lo = ilo;
+            t.out_hi = ihi;
+            inner.push_back(t);
+            raw.push_back(band);
+            raw.push_back(inner);
+            e->overlap = true;
         }
         e->user_regions.push_back({e->Hx, e->row0, 0, e->R});
         e->load_regions = e->user_regions;
@@ -399,7 +461,7 @@ gol_status get_event(gol_engine* e, hipEvent_t* ev)
     return GOL_OK;
 }
 
-gol_status launch(gol_engine* e, int plan, uint32_t depth)
+gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true)
 {
     const auto& p = e->plans[plan];
     StepArgs a{};
@@ -427,13 +489,12 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth)
     if (timed) {
         HIP_TRY(hipEventRecord(e1, e->stream));
         e->ev_pending.push_back({e0, e1});
-        double own = 0, comp = 0;
-        for (const auto& r : e->user_regions) own += (double)r.rows;
+        double comp = 0;
         for (const auto& s : p.segs) comp += (double)(s.out_hi - s.out_lo);
-        e->pending_cells.push_back(own * (double)e->W * depth);
+        e->pending_cells.push_back(p.own_rows * (double)e->W * depth);
         e->pending_cells_comp.push_back(comp * (double)e->W * depth);
     }
-    e->cur ^= 1;
+    if (swap) e->cur ^= 1;
     return GOL_OK;
 }
 
@@ -446,20 +507,19 @@ uint32_t pick_depth(uint32_t K, uint64_t remaining)
 
 // Halo exchange (replaces exchangeGridData, Parallel_Life_MPI.cpp:104-145, whose
 // receives land in copies): Hx rows each way with the up/down neighbour.
-gol_status exchange(gol_engine* e)
+gol_status exchange(gol_engine* e, hipStream_t st)
 {
     uint64_t* b = e->buf[e->cur];
     const size_t n = (size_t)e->Hx * e->stride;
     const size_t S = e->stride;
     NCCL_TRY(ncclGroupStart());
     if (e->rank > 0) {
-        NCCL_TRY(ncclSend(b + e->Hx * S, n, ncclUint64, e->rank - 1, e->comm, e->stream));
-        NCCL_TRY(ncclRecv(b, n, ncclUint64, e->rank - 1, e->comm, e->stream));
+        NCCL_TRY(ncclSend(b + e->Hx * S, n, ncclUint64, e->rank - 1, e->comm, st));
+        NCCL_TRY(ncclRecv(b, n, ncclUint64, e->rank - 1, e->comm, st));
     }
     if (e->rank < e->nranks - 1) {
-        NCCL_TRY(ncclSend(b + e->R * S, n, ncclUint64, e->rank + 1, e->comm, e->stream));
-        NCCL_TRY(ncclRecv(b + (e->R + e->Hx) * S, n, ncclUint64, e->rank + 1, e->comm,
-                          e->stream));
+        NCCL_TRY(ncclSend(b + e->R * S, n, ncclUint64, e->rank + 1, e->comm, st));
+        NCCL_TRY(ncclRecv(b + (e->R + e->Hx) * S, n, ncclUint64, e->rank + 1, e->comm, st));
     }
     NCCL_TRY(ncclGroupEnd());
     return GOL_OK;
@@ -637,11 +697,22 @@ void gol_destroy(gol_engine* e)
 {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
+    // group neighbours may still be copying from this engine's buffers
+    for (gol_engine* n : {e->up, e->down}) {
+        if (!n) continue;
+        if (n->stream) (void)hipStreamSynchronize(n->stream);
+        if (n->comm_stream) (void)hipStreamSynchronize(n->comm_stream);
+    }
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->up) e->up->down = nullptr;
     if (e->down) e->down->up = nullptr;
     if (e->ev_ready) (void)hipEventDestroy(e->ev_ready);
     if (e->ev_copied) (void)hipEventDestroy(e->ev_copied);
+    if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
+    if (e->ev_band) (void)hipEventDestroy(e->ev_band);
+    if (e->ev_xdone) (void)hipEventDestroy(e->ev_xdone);
+    if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
     for (auto& p : e->plans)
         if (p.dev) (void)hipFree(p.dev);
     for (int b = 0; b < 2; ++b)
@@ -678,6 +749,9 @@ static uint64_t load_rows_needed(const gol_engine* e)
 static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs, bool canonical)
 {
     HIP_TRY(hipSetDevice(e->device));
+    if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->halo_fresh = false;
     // clear everything (halos, unused rows) then copy each region, masking pad bits
     const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
     HIP_TRY(hipMemsetAsync(e->alloc[e->cur], 0, words_all * 8, e->stream));
@@ -770,6 +844,9 @@ gol_status gol_init_random(gol_engine* e, uint64_t seed)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
     HIP_TRY(hipSetDevice(e->device));
+    if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->halo_fresh = false;
     const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
     HIP_TRY(hipMemsetAsync(e->alloc[e->cur], 0, words_all * 8, e->stream));
     for (const auto& r : e->load_regions)
@@ -787,42 +864,75 @@ namespace {
 // The launches of one round of `round` generations after a halo exchange: each
 // launch of depth d shrinks the valid region by d rows per side (plan c-1 for a
 // cumulative shrink of c).
-gol_status run_round(gol_engine* e, uint64_t round)
+// The launches of one round of `round` generations after a halo exchange: each
+// launch of depth d shrinks the valid region by d rows per side (plan c-1 for a
+// cumulative shrink of c).  With overlap, the last launch of a full round runs
+// as band + interior and `xchg` (the transport) is called between them; it must
+// start the next round's exchange on e->comm_stream after e->ev_band.
+template <class Xchg>
+gol_status run_round(gol_engine* e, uint64_t round, Xchg&& xchg)
 {
     uint64_t done = 0;
     while (done < round) {
         const uint32_t d = pick_depth(e->K, round - done);
         done += d;
-        gol_status st = launch(e, (int)(done - 1), d);
+        gol_status st;
+        if (e->overlap && done == e->Hx) {
+            st = launch(e, (int)e->Hx, d, false);  // band rows first
+            if (st != GOL_OK) return st;
+            HIP_TRY(hipEventRecord(e->ev_band, e->stream));
+            st = launch(e, (int)e->Hx + 1, d, false);  // interior, overlaps the exchange
+            if (st != GOL_OK) return st;
+            e->cur ^= 1;
+            st = xchg();
+            if (st != GOL_OK) return st;
+            e->halo_fresh = true;
+        } else {
+            st = launch(e, (int)(done - 1), d);
+        }
         if (st != GOL_OK) return st;
     }
     return GOL_OK;
 }
 
-// Loopback exchange of a group member: pull the neighbours' boundary rows into
-// this engine's halo rows (same layout as the RCCL exchange).
-gol_status pull_halos(gol_engine* e)
+// Loopback exchange of a group member on stream `st`: pull the neighbours'
+// boundary rows into this engine's halo rows (same layout as the RCCL exchange).
+// `ready` names the neighbour event after which those rows are final.
+gol_status pull_halos(gol_engine* e, hipStream_t st, hipEvent_t gol_engine::*ready)
 {
     const size_t S = e->stride, n = (size_t)e->Hx * S * sizeof(uint64_t);
     uint64_t* b = e->buf[e->cur];
     if (gol_engine* u = e->up) {
-        HIP_TRY(hipStreamWaitEvent(e->stream, u->ev_ready, 0));
+        HIP_TRY(hipStreamWaitEvent(st, u->*ready, 0));
         const uint64_t* src = u->buf[u->cur] + u->R * S;  // its last Hx own rows
         if (u->device == e->device)
-            HIP_TRY(hipMemcpyAsync(b, src, n, hipMemcpyDeviceToDevice, e->stream));
+            HIP_TRY(hipMemcpyAsync(b, src, n, hipMemcpyDeviceToDevice, st));
         else
-            HIP_TRY(hipMemcpyPeerAsync(b, e->device, src, u->device, n, e->stream));
+            HIP_TRY(hipMemcpyPeerAsync(b, e->device, src, u->device, n, st));
     }
     if (gol_engine* d = e->down) {
-        HIP_TRY(hipStreamWaitEvent(e->stream, d->ev_ready, 0));
+        HIP_TRY(hipStreamWaitEvent(st, d->*ready, 0));
         const uint64_t* src = d->buf[d->cur] + d->Hx * S;  // its first Hx own rows
         uint64_t* dst = b + (e->R + e->Hx) * S;
         if (d->device == e->device)
-            HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, e->stream));
+            HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st));
         else
-            HIP_TRY(hipMemcpyPeerAsync(dst, e->device, src, d->device, n, e->stream));
+            HIP_TRY(hipMemcpyPeerAsync(dst, e->device, src, d->device, n, st));
     }
-    HIP_TRY(hipEventRecord(e->ev_copied, e->stream));
+    return GOL_OK;
+}
+
+// Make the compute stream wait for an overlapped exchange issued at the end of
+// the previous round (own halo rows received; for groups also the neighbours'
+// pulls of my band rows, which my next launches overwrite).
+gol_status wait_fresh_halos(gol_engine* e)
+{
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_xdone, 0));
+    if (e->grouped) {
+        if (e->up) HIP_TRY(hipStreamWaitEvent(e->stream, e->up->ev_xdone, 0));
+        if (e->down) HIP_TRY(hipStreamWaitEvent(e->stream, e->down->ev_xdone, 0));
+    }
+    e->halo_fresh = false;
     return GOL_OK;
 }
 
@@ -837,10 +947,17 @@ gol_status gol_step(gol_engine* e, uint64_t generations)
     HIP_TRY(hipSetDevice(e->device));
     uint64_t left = generations;
     if (e->nranks > 1) {
+        auto xchg = [e]() -> gol_status {  // overlapped: on comm after the band launch
+            HIP_TRY(hipStreamWaitEvent(e->comm_stream, e->ev_band, 0));
+            gol_status st = exchange(e, e->comm_stream);
+            if (st != GOL_OK) return st;
+            HIP_TRY(hipEventRecord(e->ev_xdone, e->comm_stream));
+            return GOL_OK;
+        };
         while (left > 0) {
             const uint64_t round = std::min<uint64_t>(left, e->Hx);
-            gol_status st = exchange(e);
-            if (st == GOL_OK) st = run_round(e, round);
+            gol_status st = e->halo_fresh ? wait_fresh_halos(e) : exchange(e, e->stream);
+            if (st == GOL_OK) st = run_round(e, round, xchg);
             if (st != GOL_OK) return st;
             left -= round;
         }
@@ -868,23 +985,54 @@ gol_status gol_group_step(gol_engine** engines, int nranks, uint64_t generations
     uint64_t left = generations;
     while (left > 0) {
         const uint64_t round = std::min<uint64_t>(left, Hx);
-        for (int r = 0; r < nranks; ++r) {  // every member's state is final
-            gol_engine* e = engines[r];
-            HIP_TRY(hipSetDevice(e->device));
-            HIP_TRY(hipEventRecord(e->ev_ready, e->stream));
+        if (!engines[0]->halo_fresh) {
+            // blocking exchange on the compute streams (first round after a load)
+            for (int r = 0; r < nranks; ++r) {  // every member's state is final
+                gol_engine* e = engines[r];
+                HIP_TRY(hipSetDevice(e->device));
+                HIP_TRY(hipEventRecord(e->ev_ready, e->stream));
+            }
+            for (int r = 0; r < nranks; ++r) {
+                gol_engine* e = engines[r];
+                HIP_TRY(hipSetDevice(e->device));
+                gol_status st = pull_halos(e, e->stream, &gol_engine::ev_ready);
+                if (st != GOL_OK) return st;
+                HIP_TRY(hipEventRecord(e->ev_copied, e->stream));
+            }
+            for (int r = 0; r < nranks; ++r) {  // neighbours done reading my rows
+                gol_engine* e = engines[r];
+                HIP_TRY(hipSetDevice(e->device));
+                if (e->up) HIP_TRY(hipStreamWaitEvent(e->stream, e->up->ev_copied, 0));
+                if (e->down) HIP_TRY(hipStreamWaitEvent(e->stream, e->down->ev_copied, 0));
+            }
+        } else {
+            for (int r = 0; r < nranks; ++r) {
+                HIP_TRY(hipSetDevice(engines[r]->device));
+                gol_status st = wait_fresh_halos(engines[r]);
+                if (st != GOL_OK) return st;
+            }
         }
+        // launches; the overlapped pulls are issued once every member has
+        // recorded its band event (the lambda only marks the member ready)
+        bool pulls_due = false;
         for (int r = 0; r < nranks; ++r) {
-            HIP_TRY(hipSetDevice(engines[r]->device));
-            gol_status st = pull_halos(engines[r]);
-            if (st != GOL_OK) return st;
-        }
-        for (int r = 0; r < nranks; ++r) {  // neighbours done reading my rows
             gol_engine* e = engines[r];
             HIP_TRY(hipSetDevice(e->device));
-            if (e->up) HIP_TRY(hipStreamWaitEvent(e->stream, e->up->ev_copied, 0));
-            if (e->down) HIP_TRY(hipStreamWaitEvent(e->stream, e->down->ev_copied, 0));
-            gol_status st = run_round(e, round);
+            gol_status st = run_round(e, round, [&pulls_due]() -> gol_status {
+                pulls_due = true;
+                return GOL_OK;
+            });
             if (st != GOL_OK) return st;
+        }
+        if (pulls_due) {
+            for (int r = 0; r < nranks; ++r) {
+                gol_engine* e = engines[r];
+                HIP_TRY(hipSetDevice(e->device));
+                HIP_TRY(hipStreamWaitEvent(e->comm_stream, e->ev_band, 0));
+                gol_status st = pull_halos(e, e->comm_stream, &gol_engine::ev_band);
+                if (st != GOL_OK) return st;
+                HIP_TRY(hipEventRecord(e->ev_xdone, e->comm_stream));
+            }
         }
         left -= round;
     }
@@ -895,6 +1043,7 @@ gol_status gol_sync(gol_engine* e)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
     return GOL_OK;
 }
 

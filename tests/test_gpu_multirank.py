@@ -79,3 +79,23 @@ def test_rank_engine_single_rank(pkg, oracle):
         e.load_packed(g)
         e.step(20)
         assert (e.store_packed() == oracle.bp_run(g, w, 20, oracle.CONWAY)).all()
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_group_overlap_across_calls(pkg, oracle, nranks):
+    """Overlapped exchanges (R >= 2*halo) carried across gol_step calls, partial
+    rounds, and reset by a reload."""
+    h, w = 400, 1000
+    g = oracle.bp_random(h, w, 17)
+    with pkg.Group(h, w, nranks, rule=pkg.CONWAY, tb_depth=4, halo_depth=16) as grp:
+        grp.load_packed(g)
+        done = 0
+        for chunk in (16, 16, 5, 32, 11, 16):
+            grp.step(chunk)
+            done += chunk
+            want = oracle.bp_run(g, w, done, oracle.CONWAY)
+            assert (grp.store_packed() == want).all(), f"after {done}"
+        g2 = oracle.bp_random(h, w, 18)
+        grp.load_packed(g2)
+        grp.step(40)
+        assert (grp.store_packed() == oracle.bp_run(g2, w, 40, oracle.CONWAY)).all()
