@@ -86,7 +86,8 @@ def traffic_for(cfg):
     except Exception:
         return None
     for r in rec.get("records", []):
-        if all(r.get(k) == cfg.get(k) for k in ("size", "tb_depth", "rows_per_wave", "n_gpus")):
+        if all(r.get(k, 1) == cfg.get(k) for k in ("size", "tb_depth", "rows_per_wave", "n_gpus",
+                                                    "streams")):
             return r.get("hbm_bytes_per_launch")
     return None
 
@@ -156,9 +157,12 @@ def main():
     # dominant kernel: the fused stencil; algorithmic bytes per launch =
     # 0.25 B x (own cell-generations one launch produces)
     cg_per_launch = tm["cell_gens"] / max(tm["launches"], 1)
-    achieved = BYTES_PER_CELL_GEN * cg_per_launch / (avg_launch_ms / 1e3) / 1e9
+    # a composite engine (gol_config.streams > 1) runs that many stripe launches
+    # concurrently, each timed on its own stream: per-launch rate x streams
+    streams = max(1, tm.get("streams", 1))
+    achieved = BYTES_PER_CELL_GEN * cg_per_launch * streams / (avg_launch_ms / 1e3) / 1e9
     cfg_key = {"size": n, "tb_depth": eng.tb_depth, "rows_per_wave": a.rows_per_wave,
-               "n_gpus": world}
+               "n_gpus": world, "streams": streams}
     traffic = traffic_for(cfg_key)
 
     if rank == 0:
@@ -193,6 +197,8 @@ def main():
                 "kernel": "life_tb_kernel",
                 "avg_launch_ms": round(avg_launch_ms, 4),
                 "launches": tm["launches"],
+                "concurrent_streams": streams,
+                "achieved_wall": round(BYTES_PER_CELL_GEN * gcups, 1),
                 "cell_gens_per_launch": cg_per_launch,
                 "bytes_per_cell_gen": BYTES_PER_CELL_GEN,
             },

@@ -75,7 +75,12 @@ typedef struct gol_config {
     uint32_t kernel_variant;/* stencil state layout: 0 = auto, 1 = full (14 VGPRs
                               per fused generation), 2 = compact (10 VGPRs, +4 VALU
                               ops per word-generation) */
-    uint32_t reserved[3];
+    uint32_t streams;      /* gol_create, GLOBAL only: split the field into this
+                              many row stripes advanced on their own streams of
+                              the device (k-deep halos, device copies), so one
+                              stripe's launch tail overlaps the others' work;
+                              0 = auto (2 when h >= 32768), 1 = one stream */
+    uint32_t reserved[2];
 } gol_config;
 
 typedef struct gol_engine gol_engine;
@@ -85,6 +90,8 @@ typedef struct gol_timing {
     double kernel_ms;      /* sum of their HIP-event durations */
     double cell_gens;      /* cell-generations those launches produced (own rows) */
     double cell_gens_computed; /* including redundant halo/overlap work */
+    uint32_t streams;      /* stripe streams whose launches run concurrently */
+    uint32_t reserved;
 } gol_timing;
 
 /* Defaults: reference-effective rule, GLOBAL semantics, auto tuning. */

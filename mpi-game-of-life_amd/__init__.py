@@ -49,7 +49,8 @@ class Config(ctypes.Structure):
         ("halo_depth", ctypes.c_uint32),
         ("rows_per_wave", ctypes.c_uint32),
         ("kernel_variant", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 3),
+        ("streams", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 2),
     ]
 
 
@@ -59,6 +60,8 @@ class Timing(ctypes.Structure):
         ("kernel_ms", ctypes.c_double),
         ("cell_gens", ctypes.c_double),
         ("cell_gens_computed", ctypes.c_double),
+        ("streams", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -130,7 +133,7 @@ def _check(st):
 
 
 def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_depth=0,
-                halo_depth=0, rows_per_wave=0, kernel_variant=0):
+                halo_depth=0, rows_per_wave=0, kernel_variant=0, streams=0):
     c = Config()
     lib().gol_config_init(ctypes.byref(c))
     c.birth_mask, c.survive_mask = rule
@@ -141,6 +144,7 @@ def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_
     c.halo_depth = halo_depth
     c.rows_per_wave = rows_per_wave
     c.kernel_variant = kernel_variant
+    c.streams = streams
     return c
 
 
@@ -161,11 +165,11 @@ class Engine:
 
     def __init__(self, h, w, rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1,
                  tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None,
-                 kernel_variant=0, _handle=None):
+                 kernel_variant=0, streams=0, _handle=None):
         self.h, self.w = h, w
         self.wq = (w + 63) // 64
         cfg = make_config(rule, device, semantics, ref_ranks, tb_depth, halo_depth,
-                          rows_per_wave, kernel_variant)
+                          rows_per_wave, kernel_variant, streams)
         handle = ctypes.c_void_p()
         if _handle is not None:
             handle = _handle
@@ -248,7 +252,7 @@ class Engine:
         t = Timing()
         _check(lib().gol_get_timing(self._h, ctypes.byref(t)))
         return {"launches": t.launches, "kernel_ms": t.kernel_ms, "cell_gens": t.cell_gens,
-                "cell_gens_computed": t.cell_gens_computed}
+                "cell_gens_computed": t.cell_gens_computed, "streams": t.streams}
 
 
 class Group:

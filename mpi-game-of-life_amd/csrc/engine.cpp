@@ -25,6 +25,11 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// gol_create splits GLOBAL fields of at least this many rows into 2 same-device
+// stripes on 2 streams (measured +11% at 65536^2; no gain at <= 16384 rows,
+// profiles/r01/group_bench_*.jsonl)
+constexpr uint64_t kCompositeMinRows = 32768;
+
 gol_status fail(gol_status st, const std::string& msg)
 {
     g_last_error = msg;
@@ -162,6 +167,11 @@ struct gol_engine {
     hipEvent_t ev_band = nullptr, ev_xdone = nullptr;
     bool overlap = false;
     bool halo_fresh = false;
+
+    // composite engine (gol_create, large GLOBAL fields): the field is S row
+    // stripes on S streams of this device (a gol_create_group), so one stripe's
+    // launch tail overlaps the others' work; every call is routed to the parts
+    std::vector<gol_engine*> parts;
 
     uint64_t buf_rows = 0;
     uint64_t* alloc[2] = {nullptr, nullptr};
@@ -553,6 +563,37 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
     gol_engine* e = new (std::nothrow) gol_engine();
     if (!e) return fail(GOL_ENOMEM, "host allocation");
     e->R = h;
+    uint32_t S = cfg->streams;
+    if (S == 0) S = (cfg->semantics == GOL_SEM_GLOBAL && h >= kCompositeMinRows) ? 2 : 1;
+    if (S > 1 && cfg->semantics == GOL_SEM_GLOBAL && h / S >= 256) {
+        // composite: S same-device stripes with deep halos, advanced together
+        gol_config c = *cfg;
+        c.streams = 1;
+        if (!c.halo_depth) c.halo_depth = 16 * (c.tb_depth ? c.tb_depth : 8);
+        int dev = cfg->device;
+        if (dev < 0) {
+            hipError_t he = hipGetDevice(&dev);
+            if (he != hipSuccess) {
+                delete e;
+                return fail(GOL_EHIP, std::string("hipGetDevice: ") + hipGetErrorString(he));
+            }
+        }
+        std::vector<int> devs(S, dev);
+        e->parts.assign(S, nullptr);
+        st = gol_create_group(h, w, &c, (int)S, devs.data(), e->parts.data());
+        if (st != GOL_OK) {
+            e->parts.clear();
+            delete e;
+            return st;
+        }
+        e->H = h;
+        e->W = w;
+        e->wq = (w + 63) / 64;
+        e->device = dev;
+        e->K = e->parts[0]->K;
+        *out = e;
+        return GOL_OK;
+    }
     st = init_common(e, h, w, cfg);
     if (st != GOL_OK) {
         std::string msg = g_last_error;
@@ -696,6 +737,12 @@ gol_status gol_create_group(uint64_t h, uint64_t w, const gol_config* cfg, int n
 void gol_destroy(gol_engine* e)
 {
     if (!e) return;
+    if (!e->parts.empty()) {
+        for (auto* p : e->parts) (void)hipStreamSynchronize(p->stream);
+        for (auto* p : e->parts) gol_destroy(p);
+        delete e;
+        return;
+    }
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
     // group neighbours may still be copying from this engine's buffers
@@ -796,11 +843,26 @@ static gol_status download(gol_engine* e, uint64_t* words, uint64_t rs, bool can
     return GOL_OK;
 }
 
+// composite engines: part r holds field rows [row0_r, row0_r + rows_r)
+static void part_rows(const gol_engine* e, size_t r, uint64_t* row0, uint64_t* rows)
+{
+    gol_rank_rows(e->H, (int)e->parts.size(), (int)r, row0, rows);
+}
+
 extern "C" {
 
 gol_status gol_load_packed(gol_engine* e, const uint64_t* words, uint64_t rs)
 {
     if (!e || !words) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) {
+        for (size_t r = 0; r < e->parts.size(); ++r) {
+            uint64_t r0, n;
+            part_rows(e, r, &r0, &n);
+            gol_status st = gol_load_packed(e->parts[r], words + r0 * rs, rs);
+            if (st != GOL_OK) return st;
+        }
+        return GOL_OK;
+    }
     if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
     return upload(e, words, rs, true);
 }
@@ -808,6 +870,18 @@ gol_status gol_load_packed(gol_engine* e, const uint64_t* words, uint64_t rs)
 gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
 {
     if (!e || !buf) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) {
+        if (len != e->H * (e->W + 1))
+            return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
+                                        std::to_string(e->H * (e->W + 1)));
+        for (size_t r = 0; r < e->parts.size(); ++r) {
+            uint64_t r0, n;
+            part_rows(e, r, &r0, &n);
+            gol_status st = gol_load_ascii(e->parts[r], buf + r0 * (e->W + 1), n * (e->W + 1));
+            if (st != GOL_OK) return st;
+        }
+        return GOL_OK;
+    }
     const uint64_t rows = load_rows_needed(e);
     if (len != rows * (e->W + 1))
         return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
@@ -822,6 +896,15 @@ gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
 gol_status gol_store_packed(gol_engine* e, uint64_t* words, uint64_t rs)
 {
     if (!e || !words) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) {
+        for (size_t r = 0; r < e->parts.size(); ++r) {
+            uint64_t r0, n;
+            part_rows(e, r, &r0, &n);
+            gol_status st = gol_store_packed(e->parts[r], words + r0 * rs, rs);
+            if (st != GOL_OK) return st;
+        }
+        return GOL_OK;
+    }
     if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
     return download(e, words, rs, true);
 }
@@ -829,6 +912,18 @@ gol_status gol_store_packed(gol_engine* e, uint64_t* words, uint64_t rs)
 gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
 {
     if (!e || !buf) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) {
+        if (len != e->H * (e->W + 1))
+            return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
+                                        std::to_string(e->H * (e->W + 1)));
+        for (size_t r = 0; r < e->parts.size(); ++r) {
+            uint64_t r0, n;
+            part_rows(e, r, &r0, &n);
+            gol_status st = gol_store_ascii(e->parts[r], buf + r0 * (e->W + 1), n * (e->W + 1));
+            if (st != GOL_OK) return st;
+        }
+        return GOL_OK;
+    }
     const uint64_t rows = user_rows(e);
     if (len != rows * (e->W + 1))
         return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
@@ -843,6 +938,13 @@ gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
 gol_status gol_init_random(gol_engine* e, uint64_t seed)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) {
+        for (auto* p : e->parts) {
+            gol_status st = gol_init_random(p, seed);
+            if (st != GOL_OK) return st;
+        }
+        return GOL_OK;
+    }
     HIP_TRY(hipSetDevice(e->device));
     if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -943,6 +1045,7 @@ extern "C" {
 gol_status gol_step(gol_engine* e, uint64_t generations)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) return gol_group_step(e->parts.data(), (int)e->parts.size(), generations);
     if (e->grouped) return fail(GOL_ESTATE, "group members advance with gol_group_step");
     HIP_TRY(hipSetDevice(e->device));
     uint64_t left = generations;
@@ -1042,6 +1145,13 @@ gol_status gol_group_step(gol_engine** engines, int nranks, uint64_t generations
 gol_status gol_sync(gol_engine* e)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) {
+        for (auto* p : e->parts) {
+            gol_status st = gol_sync(p);
+            if (st != GOL_OK) return st;
+        }
+        return GOL_OK;
+    }
     HIP_TRY(hipStreamSynchronize(e->stream));
     if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
     return GOL_OK;
@@ -1050,6 +1160,19 @@ gol_status gol_sync(gol_engine* e)
 gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
 {
     if (!e || !live || !hash) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) {
+        uint64_t L = 0, Hs = 0;
+        for (auto* p : e->parts) {
+            uint64_t l, h;
+            gol_status st = gol_digest(p, &l, &h);
+            if (st != GOL_OK) return st;
+            L += l;
+            Hs += h;
+        }
+        *live = L;
+        *hash = Hs;
+        return GOL_OK;
+    }
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemsetAsync(e->d_acc, 0, 2 * sizeof(unsigned long long), e->stream));
     for (const auto& r : e->user_regions)
@@ -1067,6 +1190,13 @@ gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
 gol_status gol_set_timing(gol_engine* e, int every)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) {
+        for (auto* p : e->parts) {
+            gol_status st = gol_set_timing(p, every);
+            if (st != GOL_OK) return st;
+        }
+        return GOL_OK;
+    }
     if (every < 0) return fail(GOL_EINVAL, "timing sample interval must be >= 0");
     e->timing_every = (uint32_t)every;
     e->launch_count = 0;
@@ -1076,15 +1206,38 @@ gol_status gol_set_timing(gol_engine* e, int every)
 gol_status gol_get_timing(gol_engine* e, gol_timing* out)
 {
     if (!e || !out) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) {
+        gol_timing t{};
+        for (auto* p : e->parts) {
+            gol_timing pt{};
+            gol_status st = gol_get_timing(p, &pt);
+            if (st != GOL_OK) return st;
+            t.launches += pt.launches;
+            t.kernel_ms += pt.kernel_ms;
+            t.cell_gens += pt.cell_gens;
+            t.cell_gens_computed += pt.cell_gens_computed;
+        }
+        t.streams = (uint32_t)e->parts.size();
+        *out = t;
+        return GOL_OK;
+    }
     gol_status st = flush_timing(e);
     if (st != GOL_OK) return st;
     *out = e->tm;
+    out->streams = 1;
     return GOL_OK;
 }
 
 gol_status gol_reset_timing(gol_engine* e)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) {
+        for (auto* p : e->parts) {
+            gol_status st = gol_reset_timing(p);
+            if (st != GOL_OK) return st;
+        }
+        return GOL_OK;
+    }
     gol_status st = flush_timing(e);
     if (st != GOL_OK) return st;
     e->tm = gol_timing{};
@@ -1094,6 +1247,16 @@ gol_status gol_reset_timing(gol_engine* e)
 gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uint64_t* rows,
                     uint32_t* tb_depth, uint32_t* halo_depth, uint32_t* rows_per_wave)
 {
+    if (e && !e->parts.empty()) {
+        gol_status st = gol_info(e->parts[0], nullptr, nullptr, nullptr, nullptr, tb_depth,
+                                 halo_depth, rows_per_wave);
+        if (st != GOL_OK) return st;
+        if (h) *h = e->H;
+        if (w) *w = e->W;
+        if (row0) *row0 = 0;
+        if (rows) *rows = e->H;
+        return GOL_OK;
+    }
     if (e && rows_per_wave) *rows_per_wave = e->plans.empty() ? 0 : (uint32_t)e->plans.back().rpw;
     if (!e) return fail(GOL_EINVAL, "null engine");
     if (h) *h = e->H;

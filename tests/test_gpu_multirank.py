@@ -99,3 +99,29 @@ def test_group_overlap_across_calls(pkg, oracle, nranks):
         grp.load_packed(g2)
         grp.step(40)
         assert (grp.store_packed() == oracle.bp_run(g2, w, 40, oracle.CONWAY)).all()
+
+
+@pytest.mark.parametrize("streams", [2, 3])
+def test_composite_engine(pkg, oracle, ref_data, streams):
+    """gol_create with streams = S: the field as S same-device stripes on S streams,
+    behind the single-engine API (load/step/store/digest/timing)."""
+    h, w = 1100, 777
+    g = oracle.bp_random(h, w, 23)
+    with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, streams=streams, tb_depth=8) as e:
+        assert (e.rows, e.row0) == (h, 0)
+        e.load_packed(g)
+        e.set_timing(1)
+        for chunk in (7, 64, 129):
+            e.step(chunk)
+        e.sync()
+        want = oracle.bp_run(g, w, 200, oracle.CONWAY)
+        assert (e.store_packed() == want).all()
+        assert e.digest() == oracle.bp_digest(want, w)
+        t = e.timing()
+        assert t["streams"] == streams and t["launches"] > 0
+    gold = json.load(open(os.path.join(GOLDEN, "ref_outputs.json")))
+    case = [c for c in gold["cases"] if c["np"] == 1 and c["gens"] == 100][0]
+    with pkg.Engine(1500, 500, device=0, streams=streams) as e:
+        e.load_ascii(ref_data)
+        e.step(100)
+        assert hashlib.sha256(e.store_ascii()).hexdigest() == case["sha256"]

@@ -36,6 +36,7 @@ def main():
     p.add_argument("--rows-per-wave", type=int, default=0)
     p.add_argument("--out", default="profiles/traffic.json")
     p.add_argument("--tag", default="")
+    p.add_argument("--streams", type=int, default=2, help="engine stripe streams when profiled")
     a = p.parse_args()
     fetch = per_kernel(os.path.join(a.prof_dir, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"),
                        "FETCH_SIZE")
@@ -44,21 +45,26 @@ def main():
     n = a.size
     wq = (n + 63) // 64
     stride = (wq + 7) // 8 * 8
-    digest_bytes = n * wq * 8
-    init_bytes = n * stride * 8
+    # with a composite engine every part runs its own digest / init over 1/streams
+    # of the rows (the tool profiles the default engine of tools/profile_run.py)
+    digest_bytes = n * wq * 8 / a.streams
+    init_bytes = n * stride * 8 / a.streams
     f_read = digest_bytes / statistics.mean(fetch["digest_kernel"])
     f_write = init_bytes / statistics.mean(write["init_random_kernel"])
     rd = statistics.mean(fetch["life_tb_kernel"]) * f_read
     wr = statistics.mean(write["life_tb_kernel"]) * f_write
     cells = n * n
+    launches = len(fetch["life_tb_kernel"])
     rec = {
         "size": n, "tb_depth": a.tb_depth, "rows_per_wave": a.rows_per_wave, "n_gpus": 1,
+        "streams": a.streams,
         "hbm_bytes_per_launch": round(rd + wr),
         "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
         "field_bytes": cells // 8,
-        "bytes_per_cell_gen_measured": round((rd + wr) / (cells * a.tb_depth), 5),
+        # each launch covers 1/streams of the field
+        "bytes_per_cell_gen_measured": round((rd + wr) * a.streams / (cells * a.tb_depth), 5),
         "fetch_size_calibration": round(f_read, 4), "write_size_calibration": round(f_write, 4),
-        "launches_profiled": len(fetch["life_tb_kernel"]),
+        "launches_profiled": launches,
         "source": os.path.basename(os.path.normpath(a.prof_dir)) + (f" {a.tag}" if a.tag else ""),
     }
     doc = {"records": []}
@@ -66,7 +72,7 @@ def main():
         doc = json.load(open(a.out))
     doc["records"] = [r for r in doc["records"]
                       if not all(r.get(k) == rec[k] for k in ("size", "tb_depth", "rows_per_wave",
-                                                              "n_gpus"))]
+                                                              "n_gpus", "streams"))]
     doc["records"].append(rec)
     doc["_doc"] = ("HBM bytes per life_tb_kernel launch from rocprofv3 FETCH_SIZE / WRITE_SIZE "
                    "(separate passes), calibrated on digest_kernel / init_random_kernel in the "
