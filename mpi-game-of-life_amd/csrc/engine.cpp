@@ -11,7 +11,6 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/gol.h"
@@ -73,58 +72,14 @@ bool ref_stripe(uint64_t h, uint64_t P, uint64_t r, uint64_t* start, uint64_t* r
     return true;
 }
 
-// Pack `rows` ASCII lines (w cells + '\n') into `stride`-word rows; threaded.
-bool pack_ascii(const char* buf, uint64_t rows, uint64_t w, uint64_t stride, uint64_t* dst)
-{
-    const uint64_t wq = (w + 63) / 64;
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (rows * w < (1u << 20)) nt = 1;
-    std::vector<std::thread> th;
-    std::vector<char> bad(nt, 0);
-    for (unsigned t = 0; t < nt; ++t) {
-        th.emplace_back([=, &bad]() {
-            const uint64_t r0 = rows * t / nt, r1 = rows * (t + 1) / nt;
-            for (uint64_t r = r0; r < r1; ++r) {
-                const char* line = buf + r * (w + 1);
-                if (line[w] != '\n') bad[t] = 1;
-                uint64_t* out = dst + r * stride;
-                for (uint64_t q = 0; q < stride; ++q) {
-                    uint64_t v = 0;
-                    if (q < wq) {
-                        const uint64_t c0 = q * 64, n = std::min<uint64_t>(64, w - c0);
-                        for (uint64_t j = 0; j < n; ++j)
-                            v |= (uint64_t)(line[c0 + j] == '1') << gol_split_bit((unsigned)j);
-                    }
-                    out[q] = v;
-                }
-            }
-        });
+// Scoped device allocation (staging for the ASCII codec).
+struct DeviceBytes {
+    char* p = nullptr;
+    ~DeviceBytes()
+    {
+        if (p) (void)hipFree(p);
     }
-    for (auto& x : th) x.join();
-    for (char b : bad)
-        if (b) return false;
-    return true;
-}
-
-void unpack_ascii(const uint64_t* src, uint64_t rows, uint64_t w, uint64_t stride, char* buf)
-{
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (rows * w < (1u << 20)) nt = 1;
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t) {
-        th.emplace_back([=]() {
-            const uint64_t r0 = rows * t / nt, r1 = rows * (t + 1) / nt;
-            for (uint64_t r = r0; r < r1; ++r) {
-                char* line = buf + r * (w + 1);
-                const uint64_t* in = src + r * stride;
-                for (uint64_t c = 0; c < w; ++c)
-                    line[c] = ((in[c >> 6] >> gol_split_bit((unsigned)(c & 63))) & 1) ? '1' : '0';
-                line[w] = '\n';
-            }
-        });
-    }
-    for (auto& x : th) x.join();
-}
+};
 
 // A host-visible region of the field: buffer rows [buf_row, buf_row+rows) are field
 // rows [glob_row, glob_row+rows); it corresponds to the caller's ASCII/packed rows
@@ -193,6 +148,7 @@ struct gol_engine {
     std::vector<Region> load_regions;  // rows loaded (REF_STRIPES loads overlaps too)
 
     unsigned long long* d_acc = nullptr;
+    int* d_flag = nullptr;  // ASCII codec error flag
 
     // timing: HIP events around every `timing_every`-th stencil launch (0 = off)
     uint32_t timing_every = 0;
@@ -434,6 +390,7 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->buf[b] = e->alloc[b] + (size_t)gol::kGuardRows * e->stride;
     }
     HIP_TRY(hipMalloc(&e->d_acc, 2 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&e->d_flag, sizeof(int)));
     gol_status st = build_plans(e, raw);
     if (st != GOL_OK) return st;
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -765,6 +722,7 @@ void gol_destroy(gol_engine* e)
     for (int b = 0; b < 2; ++b)
         if (e->alloc[b]) (void)hipFree(e->alloc[b]);
     if (e->d_acc) (void)hipFree(e->d_acc);
+    if (e->d_flag) (void)hipFree(e->d_flag);
     for (auto& p : e->ev_pending) {
         (void)hipEventDestroy(p.first);
         (void)hipEventDestroy(p.second);
@@ -887,10 +845,29 @@ gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
         return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
                                     std::to_string(rows * (e->W + 1)) + ", got " +
                                     std::to_string(len));
-    std::vector<uint64_t> packed((size_t)rows * e->stride);
-    if (!pack_ascii(buf, rows, e->W, e->stride, packed.data()))
-        return fail(GOL_EINVAL, "malformed ASCII: a line is not w cells followed by '\\n'");
-    return upload(e, packed.data(), e->stride, false);
+    // raw bytes to the device, packed there by the ASCII codec kernel
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->halo_fresh = false;
+    DeviceBytes bytes;
+    HIP_TRY(hipMalloc(&bytes.p, len));
+    HIP_TRY(hipMemcpyAsync(bytes.p, buf, len, hipMemcpyHostToDevice, e->stream));
+    const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
+    HIP_TRY(hipMemsetAsync(e->alloc[e->cur], 0, words_all * 8, e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_flag, 0, sizeof(int), e->stream));
+    for (const auto& r : e->load_regions) {
+        const uint64_t urow = e->nranks > 1 ? 0 : r.user_row;
+        HIP_TRY(gol::launch_ascii_pack(bytes.p + urow * (e->W + 1), (int64_t)r.rows,
+                                       (int64_t)e->W, (int64_t)e->wq,
+                                       e->buf[e->cur] + r.buf_row * e->stride,
+                                       (int64_t)e->stride, e->d_flag, e->stream));
+    }
+    int bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, e->d_flag, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (bad) return fail(GOL_EINVAL, "malformed ASCII: a line is not w cells followed by '\\n'");
+    return GOL_OK;
 }
 
 gol_status gol_store_packed(gol_engine* e, uint64_t* words, uint64_t rs)
@@ -928,10 +905,17 @@ gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
     if (len != rows * (e->W + 1))
         return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
                                     std::to_string(rows * (e->W + 1)));
-    std::vector<uint64_t> packed((size_t)rows * e->stride);
-    gol_status st = download(e, packed.data(), e->stride, false);
-    if (st != GOL_OK) return st;
-    unpack_ascii(packed.data(), rows, e->W, e->stride, buf);
+    HIP_TRY(hipSetDevice(e->device));
+    DeviceBytes bytes;
+    HIP_TRY(hipMalloc(&bytes.p, len));
+    for (const auto& r : e->user_regions) {
+        const uint64_t urow = e->nranks > 1 ? 0 : r.user_row;
+        HIP_TRY(gol::launch_ascii_unpack(e->buf[e->cur] + r.buf_row * e->stride,
+                                         (int64_t)e->stride, (int64_t)r.rows, (int64_t)e->W,
+                                         (int64_t)e->wq, bytes.p + urow * (e->W + 1), e->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(buf, bytes.p, len, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     return GOL_OK;
 }
 

@@ -69,6 +69,14 @@ hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_
                               int64_t row_base, int64_t glob_row0, int64_t nrows,
                               uint64_t seed, hipStream_t s);
 
+// ASCII codec: `rows` lines of w cell bytes + '\n' (device memory) <-> column-split
+// words at dst/src with `stride` words per row.  *bad is set if a line does not
+// end in '\n' at byte w.
+hipError_t launch_ascii_pack(const char* src, int64_t rows, int64_t w, int64_t wq, uint64_t* dst,
+                             int64_t stride, int* bad, hipStream_t s);
+hipError_t launch_ascii_unpack(const uint64_t* src, int64_t stride, int64_t rows, int64_t w,
+                               int64_t wq, char* dst, hipStream_t s);
+
 // Adds popcount and hash of buffer rows [row_base, row_base+nrows) (field rows
 // glob_row0..) into acc[0], acc[1].
 hipError_t launch_digest(const uint64_t* buf, int64_t stride, int64_t wq, int64_t row_base,

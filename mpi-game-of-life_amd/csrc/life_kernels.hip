@@ -400,6 +400,50 @@ __global__ __launch_bounds__(256) void digest_kernel(const uint64_t* buf, int64_
     }
 }
 
+// ASCII codec (data.txt / output.txt bytes <-> column-split words), the
+// device-side replacement of readGridFromFile's parse (:91-99) and
+// writeDataToFile's serialisation (:157-164).  One wavefront per (row, word):
+// lane j reads the byte of column 64q+j (coalesced), __ballot forms the
+// canonical word, lane 0 stores it split.  Byte w of every row must be '\n'.
+__global__ __launch_bounds__(256) void ascii_pack_kernel(const char* src, int64_t rows, int64_t w,
+                                                         int64_t wq, uint64_t* dst,
+                                                         int64_t stride, int* bad)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t total = rows * wq;
+    const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t k = wave0; k < total; k += nwaves) {
+        const int64_t r = k / wq, q = k - r * wq;
+        const int64_t c = q * 64 + lane;
+        const char* line = src + r * (w + 1);
+        const bool live = c < w && line[c] == '1';
+        const uint64_t word = __ballot(live);
+        if (lane == 0) {
+            dst[r * stride + q] = gol_split64(word);
+            if (q == wq - 1 && line[w] != '\n') atomicOr(bad, 1);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void ascii_unpack_kernel(const uint64_t* src, int64_t stride,
+                                                           int64_t rows, int64_t w, int64_t wq,
+                                                           char* dst)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t total = rows * wq;
+    const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t k = wave0; k < total; k += nwaves) {
+        const int64_t r = k / wq, q = k - r * wq;
+        const uint64_t word = gol_join64(src[r * stride + q]);
+        const int64_t c = q * 64 + lane;
+        char* line = dst + r * (w + 1);
+        if (c < w) line[c] = ((word >> lane) & 1) ? '1' : '0';
+        if (q == wq - 1 && lane == 0) line[w] = '\n';
+    }
+}
+
 }  // namespace
 
 hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, bool compact, hipStream_t s)
@@ -443,6 +487,28 @@ hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(init_random_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, stride,
                        wq, lastmask, row_base, glob_row0, nrows, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_ascii_pack(const char* src, int64_t rows, int64_t w, int64_t wq, uint64_t* dst,
+                             int64_t stride, int* bad, hipStream_t s)
+{
+    if (rows <= 0) return hipSuccess;
+    int64_t blocks = (rows * wq + 3) / 4;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(ascii_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, w,
+                       wq, dst, stride, bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_ascii_unpack(const uint64_t* src, int64_t stride, int64_t rows, int64_t w,
+                               int64_t wq, char* dst, hipStream_t s)
+{
+    if (rows <= 0) return hipSuccess;
+    int64_t blocks = (rows * wq + 3) / 4;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(ascii_unpack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, stride,
+                       rows, w, wq, dst);
     return hipGetLastError();
 }
 

@@ -215,3 +215,23 @@ def test_timing_sampled(pkg):
         t = e.timing()
     assert t["launches"] == 3
     assert t["cell_gens"] == 1024 * 1024 * 24
+
+
+def test_ascii_codec_large_and_malformed(pkg, oracle):
+    """Device ASCII codec (ballot pack / coalesced unpack) on multi-word rows, and
+    a malformed line deep inside the field."""
+    h, w = 333, 4100
+    g = oracle.bp_random(h, w, 31)
+    data = oracle.bp_unpack(g, w)
+    for streams in (1, 2):
+        with pkg.Engine(h, w, device=0, streams=streams, rule=pkg.CONWAY) as e:
+            e.load_ascii(data)
+            assert (e.store_packed() == g).all()
+            assert e.store_ascii() == data
+            e.step(9)
+            assert e.store_ascii() == oracle.bp_unpack(oracle.bp_run(g, w, 9, oracle.CONWAY), w)
+            bad = bytearray(data)
+            bad[200 * (w + 1) + w] = ord("1")  # row 200 runs into row 201
+            with pytest.raises(pkg.GolError) as ei:
+                e.load_ascii(bytes(bad))
+            assert ei.value.status == pkg.GOL_EINVAL
