@@ -20,8 +20,15 @@ H, W = GOLD["h"], GOLD["w"]
 DEPTHS = [1, 2, 4, 6, 7, 8, 12, 16]
 
 
+def mask(ns):
+    return sum(1 << n for n in ns)
+
+
 def rules(oracle):
-    return {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}
+    return {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE,
+            "daynight": (mask([3, 6, 7, 8]), mask([3, 4, 6, 7, 8])),
+            "seeds": (mask([2]), 0),
+            "b0": (mask([0, 1]), mask([8]))}
 
 
 # ---------------------------------------------------------------- golden (C1)
@@ -141,6 +148,20 @@ def test_ref_stripes_conway(pkg, oracle, P):
         e.load_ascii(oracle.bp_unpack(g, w))
         e.step(12)
         assert (e.store_packed() == ref).all()
+
+
+@pytest.mark.parametrize("rule", ["daynight", "seeds", "b0"])
+def test_generic_rules(pkg, oracle, rule):
+    """GENERIC kernel path: births with 0 or 8 neighbours (the 4-bit count), a rule
+    with no survivors, and the dead border under B0 (outside cells never count)."""
+    R = rules(oracle)[rule]
+    for (h, w) in ((1, 1), (7, 65), (129, 4000)):
+        g = oracle.bp_random(h, w, h + w)
+        for depth in (1, 7, 8):
+            with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth) as e:
+                e.load_packed(g)
+                e.step(11)
+                assert (e.store_packed() == oracle.bp_run(g, w, 11, R)).all(), (h, w, depth)
 
 
 # ------------------------------------------------------------ C2: 4096^2
