@@ -12,7 +12,8 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgol.so")
+# GOL_LIB: dev-only override (A/B of kernel builds in tools/); the product loads libgol.so
+LIB_PATH = os.environ.get("GOL_LIB") or os.path.join(HERE, "libgol.so")
 CLI_PATH = os.path.join(HERE, "gol")
 
 GOL_OK, GOL_EINVAL, GOL_ENOMEM, GOL_EHIP, GOL_ERCCL, GOL_EIO, GOL_ESTATE = range(7)

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <map>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -150,6 +151,11 @@ struct gol_engine {
     unsigned long long* d_acc = nullptr;
     int* d_flag = nullptr;  // ASCII codec error flag
 
+    // single-stream engines replay a captured hipGraph of the launch sequence of a
+    // gol_step(gens) call (keyed by gens and the starting buffer), so a step of
+    // many short launches costs one graph launch of host work
+    std::map<std::pair<uint64_t, int>, std::pair<hipGraphExec_t, int>> graphs;
+
     // timing: HIP events around every `timing_every`-th stencil launch (0 = off)
     uint32_t timing_every = 0;
     uint64_t launch_count = 0;
@@ -197,9 +203,9 @@ int64_t pick_rows_per_wave(const std::vector<SegDesc>& segs, int32_t strips, int
     int64_t best_r[2] = {16, 16};
     double best[2] = {1e300, 1e300};
     for (int64_t R = std::max<int64_t>(8, K + 2); R <= std::min<int64_t>(1024, maxrows + K); ++R) {
-        std::vector<SegDesc> t = segs;
-        finish_segs(t, R, strips);
-        const int64_t units = plan_units(t, strips);
+        int64_t units = 0;
+        for (const auto& sg : segs)
+            units += strips * ((std::max<int64_t>(0, sg.out_hi - sg.out_lo) + R - 1) / R);
         const int64_t n = (units + simds - 1) / simds;
         const int64_t full = n / occ, rem = n % occ;
         const double slots =
@@ -315,8 +321,10 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         }
         // overlap plans: rows neighbours need = own rows [Hx, 2Hx) (to rank-1) and
         // [R, R+Hx) (to rank+1); interior = the rest of the own rows
+        // decided from the smallest stripe so every rank / group member agrees
+        // (balanced stripes differ by one row)
         const int64_t Hx = (int64_t)e->Hx, R = (int64_t)e->R;
-        if (R >= 2 * Hx) {
+        if ((int64_t)(h / (uint64_t)e->nranks) >= 2 * Hx) {
             SegDesc b = raw.back()[0];  // shrink Hx: out = own rows
             std::vector<SegDesc> band, inner;
             int64_t ilo = Hx, ihi = Hx + R;
@@ -721,6 +729,7 @@ void gol_destroy(gol_engine* e)
         if (p.dev) (void)hipFree(p.dev);
     for (int b = 0; b < 2; ++b)
         if (e->alloc[b]) (void)hipFree(e->alloc[b]);
+    for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.first);
     if (e->d_acc) (void)hipFree(e->d_acc);
     if (e->d_flag) (void)hipFree(e->d_flag);
     for (auto& p : e->ev_pending) {
@@ -1048,6 +1057,44 @@ gol_status gol_step(gol_engine* e, uint64_t generations)
             if (st != GOL_OK) return st;
             left -= round;
         }
+        return GOL_OK;
+    }
+    const bool graphable = e->timing_every == 0 && generations >= 4 * (uint64_t)e->K;
+    if (graphable) {
+        const auto key = std::make_pair(generations, e->cur);
+        auto it = e->graphs.find(key);
+        if (it == e->graphs.end()) {
+            hipGraph_t g = nullptr;
+            HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+            const int cur0 = e->cur;
+            gol_status st = GOL_OK;
+            while (left > 0 && st == GOL_OK) {
+                const uint32_t d = pick_depth(e->K, left);
+                st = launch(e, 0, d);
+                left -= d;
+            }
+            const hipError_t ce = hipStreamEndCapture(e->stream, &g);
+            if (st != GOL_OK) {
+                if (g) (void)hipGraphDestroy(g);
+                e->cur = cur0;
+                return st;
+            }
+            if (ce != hipSuccess) {
+                e->cur = cur0;
+                return fail(GOL_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+            }
+            hipGraphExec_t x = nullptr;
+            const hipError_t ie = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ie != hipSuccess) {
+                e->cur = cur0;
+                return fail(GOL_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+            }
+            it = e->graphs.emplace(key, std::make_pair(x, e->cur)).first;
+            e->cur = cur0;
+        }
+        HIP_TRY(hipGraphLaunch(it->second.first, e->stream));
+        e->cur = it->second.second;
         return GOL_OK;
     }
     while (left > 0) {

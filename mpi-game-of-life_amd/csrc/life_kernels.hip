@@ -199,6 +199,10 @@ struct StageOf<true> {
 };
 
 constexpr int kPrefetch = 4;
+#ifndef GOL_DIAGONAL
+#define GOL_DIAGONAL 1
+#endif
+constexpr bool kDiagonal = GOL_DIAGONAL;
 
 template <int K, int RULE, bool COMPACT>
 __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
@@ -287,16 +291,34 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     }
 
     for (int64_t t0 = kWarm; t0 < T; t0 += kPrefetch) {
+        u2 x[kPrefetch];
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
-            const int64_t t = t0 + p;
-            u2 x = ingest(t, ring[p]);
+            x[p] = ingest(t0 + p, ring[p]);
             ring[p] = *pf;
             pf += a.stride;
-#pragma unroll
-            for (int g = 0; g < K; ++g) x = stage(g, t, x);
-            store(t, x);
         }
+        if constexpr (kDiagonal) {
+            // stage g of step p only needs stage g-1 of step p and stage g of step
+            // p-1: issue the block's (p, g) pairs by anti-diagonal d = p + g so
+            // independent stage steps sit next to each other for the scheduler
+#pragma unroll
+            for (int d = 0; d < K + kPrefetch - 1; ++d) {
+#pragma unroll
+                for (int p = 0; p < kPrefetch; ++p) {
+                    const int g = d - p;
+                    if (g >= 0 && g < K) x[p] = stage(g, t0 + p, x[p]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < kPrefetch; ++p) {
+#pragma unroll
+                for (int g = 0; g < K; ++g) x[p] = stage(g, t0 + p, x[p]);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < kPrefetch; ++p) store(t0 + p, x[p]);
     }
 }
 

@@ -125,3 +125,15 @@ def test_composite_engine(pkg, oracle, ref_data, streams):
         e.load_ascii(ref_data)
         e.step(100)
         assert hashlib.sha256(e.store_ascii()).hexdigest() == case["sha256"]
+
+
+def test_group_overlap_uneven_stripes(pkg, oracle):
+    """Stripes of 2*halo and 2*halo-1 rows in one group: the overlap decision must
+    be the same for every member."""
+    h, w = 3 * 32 - 1, 300  # stripes 32, 32, 31 rows with halo 16
+    g = oracle.bp_random(h, w, 5)
+    with pkg.Group(h, w, 3, rule=pkg.CONWAY, tb_depth=4, halo_depth=16) as grp:
+        grp.load_packed(g)
+        for _ in range(3):
+            grp.step(16)
+        assert (grp.store_packed() == oracle.bp_run(g, w, 48, oracle.CONWAY)).all()

@@ -256,3 +256,17 @@ def test_ascii_codec_large_and_malformed(pkg, oracle):
             with pytest.raises(pkg.GolError) as ei:
                 e.load_ascii(bytes(bad))
             assert ei.value.status == pkg.GOL_EINVAL
+
+
+def test_graph_replay_matches(pkg, oracle):
+    """gol_step(gens) on a single-stream engine replays a captured hipGraph from the
+    second call on (keyed by gens and buffer parity); results stay exact."""
+    h, w = 513, 2000
+    g = oracle.bp_random(h, w, 41)
+    with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, tb_depth=4, streams=1) as e:
+        e.load_packed(g)
+        total = 0
+        for gens in (20, 20, 37, 20, 37, 37, 5):
+            e.step(gens)
+            total += gens
+            assert (e.store_packed() == oracle.bp_run(g, w, total, oracle.CONWAY)).all(), total
