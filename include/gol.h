@@ -72,9 +72,11 @@ typedef struct gol_config {
     uint32_t halo_depth;   /* multi-rank: halo rows exchanged per round
                               (= generations between exchanges); 0 = auto */
     uint32_t rows_per_wave;/* rows each wavefront streams per launch; 0 = auto */
-    uint32_t kernel_variant;/* stencil state layout: 0 = auto, 1 = full (14 VGPRs
-                              per fused generation), 2 = compact (10 VGPRs, +4 VALU
-                              ops per word-generation) */
+    uint32_t kernel_variant;/* stencil kernel: 0 = auto (= 1); 1 = full state (14
+                              VGPRs per fused generation), anti-diagonal schedule;
+                              2 = compact state (10 VGPRs, +4 VALU ops per
+                              word-generation); 3 = full state, step-major
+                              schedule (for A/B measurements) */
     uint32_t streams;      /* gol_create, GLOBAL only: split the field into this
                               many row stripes advanced on their own streams of
                               the device (k-deep halos, device copies), so one

@@ -99,7 +99,7 @@ struct gol_engine {
     gol::RuleKind rule = gol::RULE_REF;
     uint32_t K = 8;
     uint32_t rows_per_wave = 0;
-    bool compact = false;
+    int var = 0;  // stencil kernel variant (life_internal.h launch_life)
     uint32_t sem = GOL_SEM_GLOBAL;
     uint32_t P = 1;
 
@@ -224,7 +224,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
 {
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-    const int occ = std::max(1, gol::life_blocks_per_cu((int)e->K, e->rule, e->compact));
+    const int occ = std::max(1, gol::life_blocks_per_cu((int)e->K, e->rule, e->var));
     for (const auto& r : raw) {
         gol_engine::Plan p;
         p.segs = r;
@@ -265,7 +265,7 @@ gol_status check_cfg(const gol_config* cfg)
     if (cfg->tb_depth != 0 && std::find(std::begin(gol::kDepthList), std::end(gol::kDepthList),
                                         (int)cfg->tb_depth) == std::end(gol::kDepthList))
         return fail(GOL_EINVAL, "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16");
-    if (cfg->kernel_variant > 2) return fail(GOL_EINVAL, "kernel_variant must be 0, 1 or 2");
+    if (cfg->kernel_variant > 3) return fail(GOL_EINVAL, "kernel_variant must be 0..3");
     if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
     return GOL_OK;
 }
@@ -288,7 +288,7 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->rule = gol::RULE_GENERIC;
     e->K = cfg->tb_depth ? cfg->tb_depth : 8;
     e->rows_per_wave = cfg->rows_per_wave;
-    e->compact = cfg->kernel_variant == 2;
+    e->var = cfg->kernel_variant == 2 ? 1 : cfg->kernel_variant == 3 ? 2 : 0;
     e->sem = cfg->semantics;
     e->strips = (int32_t)((e->wq + gol::kStripOut - 1) / gol::kStripOut);
 
@@ -460,7 +460,7 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true)
         if (st != GOL_OK) return st;
         HIP_TRY(hipEventRecord(e0, e->stream));
     }
-    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->compact, e->stream));
+    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->var, e->stream));
     if (timed) {
         HIP_TRY(hipEventRecord(e1, e->stream));
         e->ev_pending.push_back({e0, e1});

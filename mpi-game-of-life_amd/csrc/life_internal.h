@@ -55,13 +55,15 @@ struct StepArgs {
 // Fused depths with an instantiated kernel, largest first.
 constexpr int kDepthList[] = {16, 12, 8, 7, 6, 4, 2, 1};
 
-// Launch `depth` fused generations (depth in kDepthList); `compact` selects the
-// 10-dword stage state (more waves per SIMD, 4 more VALU ops per word-generation).
-hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, bool compact, hipStream_t s);
+// Launch `depth` fused generations (depth in kDepthList).  `var` = kernel variant:
+// 0 full 14-dword stage state, anti-diagonal schedule (default); 1 compact
+// 10-dword state (+4 VALU ops per word-generation); 2 full state, step-major
+// schedule (kept for A/B measurements).
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int var, hipStream_t s);
 
 // Resident 256-thread blocks per CU of the stencil kernel for (depth, rule,
 // variant) -- each block is one wavefront per SIMD (occupancy query).
-int life_blocks_per_cu(int depth, RuleKind rule, bool compact);
+int life_blocks_per_cu(int depth, RuleKind rule, int var);
 
 // Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field
 // rows [glob_row0, glob_row0+nrows).

@@ -199,14 +199,15 @@ struct StageOf<true> {
 };
 
 constexpr int kPrefetch = 4;
-#ifndef GOL_DIAGONAL
-#define GOL_DIAGONAL 1
-#endif
-constexpr bool kDiagonal = GOL_DIAGONAL;
 
-template <int K, int RULE, bool COMPACT>
+
+// VAR: 0 = full state, 1 = compact state, 2 = full state with the plain
+// (step-major) schedule instead of the anti-diagonal one
+template <int K, int RULE, int VAR>
 __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 {
+    constexpr bool COMPACT = VAR == 1;
+    constexpr bool kDiagonal = VAR != 2;
     constexpr bool kBirths = RULE != RULE_REF;
     const int lane = threadIdx.x & 63;
     const int64_t unit =
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     }
 }
 
-template <int K, bool COMPACT>
+template <int K, int COMPACT>
 hipError_t launch_depth(const StepArgs& a, RuleKind rule, hipStream_t s)
 {
     const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
@@ -342,12 +343,16 @@ hipError_t launch_depth(const StepArgs& a, RuleKind rule, hipStream_t s)
 }
 
 template <int K>
-hipError_t launch_variant(const StepArgs& a, RuleKind rule, bool compact, hipStream_t s)
+hipError_t launch_variant(const StepArgs& a, RuleKind rule, int var, hipStream_t s)
 {
-    return compact ? launch_depth<K, true>(a, rule, s) : launch_depth<K, false>(a, rule, s);
+    switch (var) {
+    case 1: return launch_depth<K, 1>(a, rule, s);
+    case 2: return launch_depth<K, 2>(a, rule, s);
+    default: return launch_depth<K, 0>(a, rule, s);
+    }
 }
 
-template <int K, bool COMPACT>
+template <int K, int COMPACT>
 int occupancy_of(RuleKind rule)
 {
     int blocks = 0;
@@ -366,9 +371,13 @@ int occupancy_of(RuleKind rule)
 }
 
 template <int K>
-int occupancy_variant(RuleKind rule, bool compact)
+int occupancy_variant(RuleKind rule, int var)
 {
-    return compact ? occupancy_of<K, true>(rule) : occupancy_of<K, false>(rule);
+    switch (var) {
+    case 1: return occupancy_of<K, 1>(rule);
+    case 2: return occupancy_of<K, 2>(rule);
+    default: return occupancy_of<K, 0>(rule);
+    }
 }
 
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t idx)
@@ -468,7 +477,7 @@ __global__ __launch_bounds__(256) void ascii_unpack_kernel(const uint64_t* src, 
 
 }  // namespace
 
-hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, bool compact, hipStream_t s)
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int compact, hipStream_t s)
 {
     if (a.total_units <= 0) return hipSuccess;
     switch (depth) {
@@ -484,7 +493,7 @@ hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, bool compact
     }
 }
 
-int life_blocks_per_cu(int depth, RuleKind rule, bool compact)
+int life_blocks_per_cu(int depth, RuleKind rule, int compact)
 {
     switch (depth) {
     case 1: return occupancy_variant<1>(rule, compact);

@@ -82,7 +82,7 @@ def test_random_fields_every_depth(pkg, oracle, shape, rule):
     g = oracle.bp_random(h, w, seed)
     for gens in (1, 3, 16, 21):
         want[gens] = oracle.bp_run(g, w, gens, R)
-    for depth, variant in [(d, v) for d in DEPTHS for v in (1, 2)]:
+    for depth, variant in [(d, v) for d in DEPTHS for v in (1, 2, 3)]:
         for gens, ref in want.items():
             with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth,
                             kernel_variant=variant) as e:
@@ -94,7 +94,7 @@ def test_random_fields_every_depth(pkg, oracle, shape, rule):
 
 
 @pytest.mark.parametrize("rpw", [16, 32, 48, 100])
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_row_blocking(pkg, oracle, rpw, variant):
     """Many row blocks per strip (rows_per_wave small): block seams exact."""
     h, w = 300, 4100

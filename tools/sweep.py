@@ -23,6 +23,7 @@ def main():
     p.add_argument("--depths", default="4,8,16")
     p.add_argument("--rpw", default="0")
     p.add_argument("--variants", default="0")
+    p.add_argument("--streams", type=int, default=0, help="gol_config.streams (0 = auto)")
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--rule", default="ref")
     p.add_argument("--no-events", action="store_true", help="time wall clock only")
@@ -37,7 +38,7 @@ def main():
     engines = {}
     for d, r, kv in variants:
         e = pkg.Engine(h, w, rule=rule, device=0, tb_depth=d, rows_per_wave=r,
-                       kernel_variant=kv)
+                       kernel_variant=kv, streams=a.streams)
         e.init_random(1)
         e.step(d)  # warm
         e.sync()
