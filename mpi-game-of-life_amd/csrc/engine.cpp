@@ -30,6 +30,12 @@ thread_local std::string g_last_error;
 // profiles/r01/group_bench_*.jsonl)
 constexpr uint64_t kCompositeMinRows = 32768;
 
+// Auto fused depth: K = 12 for stripes of <= 24576 rows (fewer launches and the
+// anti-diagonal schedule's extra stage parallelism win where row blocks are
+// short: 79.9 vs 76.3 TCUPS at 8192x65536, 91.9 vs 88.8 at 16384x65536), K = 8
+// above (109.7 vs 108.9 at 65536^2; profiles/r01/sweep_depth_diagonal.jsonl).
+uint32_t auto_depth(uint64_t rows) { return rows <= 24576 ? 12u : 8u; }
+
 gol_status fail(gol_status st, const std::string& msg)
 {
     g_last_error = msg;
@@ -286,7 +292,7 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->rule = gol::RULE_CONWAY;
     else
         e->rule = gol::RULE_GENERIC;
-    e->K = cfg->tb_depth ? cfg->tb_depth : 8;
+    e->K = cfg->tb_depth ? cfg->tb_depth : auto_depth(e->R);
     e->rows_per_wave = cfg->rows_per_wave;
     e->var = cfg->kernel_variant == 2 ? 1 : cfg->kernel_variant == 3 ? 2 : 0;
     e->sem = cfg->semantics;
@@ -534,7 +540,7 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
         // composite: S same-device stripes with deep halos, advanced together
         gol_config c = *cfg;
         c.streams = 1;
-        if (!c.halo_depth) c.halo_depth = 16 * (c.tb_depth ? c.tb_depth : 8);
+        if (!c.halo_depth) c.halo_depth = 16 * (c.tb_depth ? c.tb_depth : auto_depth(h / S));
         int dev = cfg->device;
         if (dev < 0) {
             hipError_t he = hipGetDevice(&dev);
@@ -615,7 +621,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     e->nranks = nranks;
     e->row0 = row0;
     e->R = rows;
-    const uint32_t K = cfg->tb_depth ? cfg->tb_depth : 8;
+    const uint32_t K = cfg->tb_depth ? cfg->tb_depth : auto_depth(rows);
     // rounds of halo_depth generations between exchanges (default 8 launches)
     uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 8 * (uint64_t)K;
     if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
