@@ -30,11 +30,12 @@ thread_local std::string g_last_error;
 // profiles/r01/group_bench_*.jsonl)
 constexpr uint64_t kCompositeMinRows = 32768;
 
-// Auto fused depth: K = 12 for stripes of <= 24576 rows (fewer launches and the
+// Auto fused depth: K = 12 for stripes of <= 32768 rows (fewer launches and the
 // anti-diagonal schedule's extra stage parallelism win where row blocks are
-// short: 79.9 vs 76.3 TCUPS at 8192x65536, 91.9 vs 88.8 at 16384x65536), K = 8
-// above (109.7 vs 108.9 at 65536^2; profiles/r01/sweep_depth_diagonal.jsonl).
-uint32_t auto_depth(uint64_t rows) { return rows <= 24576 ? 12u : 8u; }
+// short: 79.9 vs 76.3 TCUPS at 8192x65536, 91.9 vs 88.8 at 16384, 97.0 vs 93.9 at
+// 32768), K = 8 above and for the composite's parts (109.7 vs 108.9 at 65536^2
+// as 2 x 32768; profiles/r01/sweep_depth_diagonal.jsonl).
+uint32_t auto_depth(uint64_t rows) { return rows <= 32768 ? 12u : 8u; }
 
 gol_status fail(gol_status st, const std::string& msg)
 {
@@ -540,7 +541,8 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
         // composite: S same-device stripes with deep halos, advanced together
         gol_config c = *cfg;
         c.streams = 1;
-        if (!c.halo_depth) c.halo_depth = 16 * (c.tb_depth ? c.tb_depth : auto_depth(h / S));
+        if (!c.tb_depth) c.tb_depth = 8;
+        if (!c.halo_depth) c.halo_depth = 16 * c.tb_depth;
         int dev = cfg->device;
         if (dev < 0) {
             hipError_t he = hipGetDevice(&dev);
