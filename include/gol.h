@@ -68,15 +68,17 @@ typedef struct gol_config {
     uint32_t semantics;    /* gol_semantics */
     uint32_t ref_ranks;    /* P for GOL_SEM_REF_STRIPES (must satisfy h >= P) */
     uint32_t tb_depth;     /* generations fused per kernel launch (temporal
-                              blocking); 0 = auto; allowed 1,2,4,6,7,8,12,16 */
+                              blocking); 0 = auto; allowed 1,2,4,6,7,8,12,16,
+                              20,24,32 */
     uint32_t halo_depth;   /* multi-rank: halo rows exchanged per round
                               (= generations between exchanges); 0 = auto */
     uint32_t rows_per_wave;/* rows each wavefront streams per launch; 0 = auto */
-    uint32_t kernel_variant;/* stencil kernel: 0 = auto (= 1); 1 = full state (14
-                              VGPRs per fused generation), anti-diagonal schedule;
-                              2 = compact state (10 VGPRs, +4 VALU ops per
-                              word-generation); 3 = full state, step-major
-                              schedule (for A/B measurements) */
+    uint32_t kernel_variant;/* stencil kernel: 0 = auto (= 1); 1 = total-sum
+                              state (9-cell sums, 10 VGPRs per fused
+                              generation), anti-diagonal schedule; 2 =
+                              neighbour-sum state (14 VGPRs, +4 VALU ops per
+                              word-generation, tb_depth <= 16); 3 = as 1 with a
+                              step-major schedule (for A/B measurements) */
     uint32_t streams;      /* gol_create, GLOBAL only: split the field into this
                               many row stripes advanced on their own streams of
                               the device (k-deep halos, device copies), so one

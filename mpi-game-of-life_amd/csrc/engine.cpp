@@ -30,12 +30,22 @@ thread_local std::string g_last_error;
 // profiles/r01/group_bench_*.jsonl)
 constexpr uint64_t kCompositeMinRows = 32768;
 
-// Auto fused depth: K = 12 for stripes of <= 32768 rows (fewer launches and the
-// anti-diagonal schedule's extra stage parallelism win where row blocks are
-// short: 79.9 vs 76.3 TCUPS at 8192x65536, 91.9 vs 88.8 at 16384, 97.0 vs 93.9 at
-// 32768), K = 8 above and for the composite's parts (109.7 vs 108.9 at 65536^2
-// as 2 x 32768; profiles/r01/sweep_depth_diagonal.jsonl).
-uint32_t auto_depth(uint64_t rows) { return rows <= 32768 ? 12u : 8u; }
+// Auto fused depth of the total-sum kernel.  K = 16 (202 VGPRs, 2 waves/SIMD,
+// enough for full VALU issue) for stripes of more than 6144 rows: 124.5 TCUPS at
+// 65536^2 vs 122.4 (K = 8, 4 waves/SIMD) and 106.0 (K = 12), 92 vs 80 / 79 at
+// 8192x65536; K >= 20 drops to 1 wave/SIMD (half issue rate) and loses 30-35%
+// (profiles/r01/sweep_total_sum_depth.jsonl).  Short fields are launch-latency
+// bound and keep K = 8 (4096^2: 11.6 vs 8.7 TCUPS at K = 16).  Rules other than
+// B/S2 and B3/S23 evaluate a 10-term mask sum whose K = 16 state spills: K = 12.
+uint32_t auto_depth(uint64_t rows, const gol_config* cfg)
+{
+    if (rows <= 6144) return 8u;
+    const bool fixed = (cfg->birth_mask == GOL_REF_BIRTH && cfg->survive_mask == GOL_REF_SURVIVE) ||
+                       (cfg->birth_mask == GOL_CONWAY_BIRTH &&
+                        cfg->survive_mask == GOL_CONWAY_SURVIVE);
+    if (cfg->kernel_variant == 2) return 12u;  // neighbour-sum state: 14 VGPRs per stage
+    return fixed ? 16u : 12u;
+}
 
 gol_status fail(gol_status st, const std::string& msg)
 {
@@ -271,8 +281,10 @@ gol_status check_cfg(const gol_config* cfg)
         return fail(GOL_EINVAL, "rule masks must be 9-bit");
     if (cfg->tb_depth != 0 && std::find(std::begin(gol::kDepthList), std::end(gol::kDepthList),
                                         (int)cfg->tb_depth) == std::end(gol::kDepthList))
-        return fail(GOL_EINVAL, "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16");
+        return fail(GOL_EINVAL, "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16,20,24,32");
     if (cfg->kernel_variant > 3) return fail(GOL_EINVAL, "kernel_variant must be 0..3");
+    if (cfg->kernel_variant == 2 && cfg->tb_depth > 16)
+        return fail(GOL_EINVAL, "kernel_variant 2 (neighbour-sum state) needs tb_depth <= 16");
     if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
     return GOL_OK;
 }
@@ -293,7 +305,7 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->rule = gol::RULE_CONWAY;
     else
         e->rule = gol::RULE_GENERIC;
-    e->K = cfg->tb_depth ? cfg->tb_depth : auto_depth(e->R);
+    e->K = cfg->tb_depth ? cfg->tb_depth : auto_depth(e->R, cfg);
     e->rows_per_wave = cfg->rows_per_wave;
     e->var = cfg->kernel_variant == 2 ? 1 : cfg->kernel_variant == 3 ? 2 : 0;
     e->sem = cfg->semantics;
@@ -541,7 +553,7 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
         // composite: S same-device stripes with deep halos, advanced together
         gol_config c = *cfg;
         c.streams = 1;
-        if (!c.tb_depth) c.tb_depth = 8;
+        if (!c.tb_depth) c.tb_depth = auto_depth(h / S, cfg);
         if (!c.halo_depth) c.halo_depth = 16 * c.tb_depth;
         int dev = cfg->device;
         if (dev < 0) {
@@ -623,7 +635,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     e->nranks = nranks;
     e->row0 = row0;
     e->R = rows;
-    const uint32_t K = cfg->tb_depth ? cfg->tb_depth : auto_depth(rows);
+    const uint32_t K = cfg->tb_depth ? cfg->tb_depth : auto_depth(rows, cfg);
     // rounds of halo_depth generations between exchanges (default 8 launches)
     uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 8 * (uint64_t)K;
     if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows

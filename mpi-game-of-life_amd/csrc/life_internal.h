@@ -36,7 +36,7 @@ constexpr int kWavesPerBlock = 4;
 // Zeroed guard rows allocated before/after every state buffer so that the
 // streaming loads (K rows of halo + prefetch distance) never leave the allocation.
 constexpr int kGuardRows = 64;
-constexpr int kMaxDepth = 16;
+constexpr int kMaxDepth = 32;
 
 struct StepArgs {
     const uint64_t* in;   // state buffer row 0 (guard rows precede it)
@@ -53,11 +53,12 @@ struct StepArgs {
 };
 
 // Fused depths with an instantiated kernel, largest first.
-constexpr int kDepthList[] = {16, 12, 8, 7, 6, 4, 2, 1};
+constexpr int kDepthList[] = {32, 24, 20, 16, 12, 8, 7, 6, 4, 2, 1};
 
 // Launch `depth` fused generations (depth in kDepthList).  `var` = kernel variant:
-// 0 full 14-dword stage state, anti-diagonal schedule (default); 1 compact
-// 10-dword state (+4 VALU ops per word-generation); 2 full state, step-major
+// 0 total-sum stage state (10 dwords per fused generation), anti-diagonal
+// schedule (default); 1 neighbour-sum state (14 dwords, +4 VALU ops per
+// word-generation; depth <= 16), anti-diagonal; 2 as 0 with the step-major
 // schedule (kept for A/B measurements).
 hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int var, hipStream_t s);
 

@@ -29,8 +29,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "bitlayout.h"
 #include "life_internal.h"
+
+#ifndef GOL_HORIZ_ADDC
+#define GOL_HORIZ_ADDC 0
+#endif
+#ifndef GOL_HORIZ_OR_DPP
+#define GOL_HORIZ_OR_DPP 0
+#endif
 
 namespace gol {
 
@@ -119,12 +128,40 @@ struct Horiz {
 };
 __device__ __forceinline__ Horiz horiz(u2 x)
 {
+#if GOL_HORIZ_ADDC
+    // left shift with the carry from lane l-1 as an add-with-carry: the carries of
+    // all lanes are one wave mask (v_cmp), moved up one lane on the scalar unit
+    const uint64_t m = __builtin_amdgcn_ballot_w64((int32_t)x.hi < 0) << 1;
+    uint32_t le;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(le), "=s"(co) : "v"(x.hi), "s"(m));
+    const uint32_t ln = lane_from_right(x.lo);
+    Horiz h;
+    h.Le = le;
+    h.Ro = __builtin_amdgcn_alignbit(ln, x.lo, 1);
+    return h;
+#elif GOL_HORIZ_OR_DPP
+    // the carry bit is shifted into place in the neighbour lane and merged by a
+    // v_or_b32 whose src0 reads it through DPP (the mov folds into the or)
+    // (the shifts are opaque asm so the compiler cannot commute them with the lane
+    // move and form a half-rate v_lshl_or_b32 instead)
+    uint32_t th, tl, sh, sl;
+    asm("v_lshrrev_b32 %0, 31, %1" : "=v"(th) : "v"(x.hi));
+    asm("v_lshlrev_b32 %0, 31, %1" : "=v"(tl) : "v"(x.lo));
+    asm("v_lshlrev_b32 %0, 1, %1" : "=v"(sh) : "v"(x.hi));
+    asm("v_lshrrev_b32 %0, 1, %1" : "=v"(sl) : "v"(x.lo));
+    Horiz h;
+    h.Le = sh | lane_from_left(th);
+    h.Ro = sl | lane_from_right(tl);
+    return h;
+#else
     const uint32_t hp = lane_from_left(x.hi);   // odd columns of word q-1 (bit 31: col 64q-1)
     const uint32_t ln = lane_from_right(x.lo);  // even columns of word q+1 (bit 0: col 64q+64)
     Horiz h;
     h.Le = __builtin_amdgcn_alignbit(x.hi, hp, 31);  // (hi << 1) | (hp >> 31)
     h.Ro = __builtin_amdgcn_alignbit(ln, x.lo, 1);   // (lo >> 1) | (ln << 31)
     return h;
+#endif
 }
 
 // One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
@@ -157,56 +194,98 @@ __device__ __forceinline__ u2 stage_step(Stage& st, u2 x, uint32_t birth, uint32
     return y;
 }
 
-// Compact stage state (10 dwords instead of 14): H3 of row r-2, H2 and cells of
-// row r-1; H3(r-1) = H2(r-1) + cells(r-1) is rebuilt (2 ops per half) when the
-// window shifts.  Trades 4 VALU ops per word-generation for 4 VGPRs per stage,
-// i.e. occupancy at larger K.
-struct StageC {
+// Total-sum stage state (10 dwords): H3 of rows r-2 and r-1 and the cells of row
+// r-1.  The emitted cell sees T = H3(r-2) + H3(r-1) + H3(r), the 9-cell sum
+// including itself, so no centre-excluded H2 is formed: 4 VALU ops per word and
+// 4 VGPRs per stage fewer than Stage.  For an alive cell T = n + 1, for a dead
+// one T = n (generic masks: survive bit T-1 / birth bit T); the two fixed rules
+// read it off directly:
+//   REF (B/S2):      next = alive && T == 3
+//   CONWAY (B3/S23): next = T == 3 || (alive && T == 4)
+struct StageT {
     u2 ps, pc;
-    u2 hs, hc;
+    u2 cs, cc;
     u2 al;
 };
-constexpr uint32_t kOrAnd = 0xF8;  // a | (b & c)
+constexpr uint32_t kAnd3 = 0x80;     // a & b & c
+constexpr uint32_t kFour = 0x42;     // ~(a ^ b) & (a ^ c)
+constexpr uint32_t kMux = 0xCA;      // a ? b : c
 
 template <int RULE>
-__device__ __forceinline__ u2 stage_step(StageC& st, u2 x, uint32_t birth, uint32_t survive)
+__device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint32_t bs,
+                                                 uint32_t bc, uint32_t es, uint32_t ec,
+                                                 uint32_t alive, uint32_t birth,
+                                                 uint32_t survive)
+{
+    // T = A + B + E, each a 2-bit H3 sum: T = s0 + 2*(p + k0) + 4*mj (0..9)
+    const uint32_t s0 = lop3<kXor3>(as, bs, es);
+    const uint32_t k0 = lop3<kMaj>(as, bs, es);
+    const uint32_t p = lop3<kXor3>(ac, bc, ec);
+    const uint32_t mj = lop3<kMaj>(ac, bc, ec);
+    // T == 3  <=>  s0 && p + k0 == 1 && !mj
+    const uint32_t three = lop3<kTwoThree>(p, k0, mj);
+    if constexpr (RULE == RULE_REF) {
+        // Parallel_Life_MPI.cpp:47-50: alive && n == 2  <=>  alive && T == 3
+        return lop3<kAnd3>(alive, s0, three);
+    } else if constexpr (RULE == RULE_CONWAY) {
+        // T == 4  <=>  !s0 && (p + k0 == 2 && !mj  ||  p + k0 == 0 && mj)
+        const uint32_t four = lop3<kFour>(p, k0, mj) & alive;
+        return lop3<kMux>(s0, three, four);
+    } else {
+        // T = s0 + 2*x + 4*t2 + 8*t3; alive cells have n = T - 1, dead ones n = T
+        const uint32_t x = p ^ k0, y = p & k0;
+        const uint32_t t2 = y ^ mj, t3 = y & mj;
+        uint32_t r = 0;
+#pragma unroll
+        for (int v = 0; v <= 9; ++v) {
+            const uint32_t ssel = v >= 1 ? (survive >> (v - 1)) & 1u : 0u;
+            const uint32_t bsel = v <= 8 ? (birth >> v) & 1u : 0u;
+            if (bsel | ssel) {
+                const uint32_t eq = ((v & 1) ? s0 : ~s0) & ((v & 2) ? x : ~x) &
+                                    ((v & 4) ? t2 : ~t2) & ((v & 8) ? t3 : ~t3);
+                const uint32_t sel = (ssel ? alive : 0u) | (bsel ? ~alive : 0u);
+                r |= eq & sel;
+            }
+        }
+        return r;
+    }
+}
+
+template <int RULE>
+__device__ __forceinline__ u2 stage_step(StageT& st, u2 x, uint32_t birth, uint32_t survive)
 {
     const Horiz hz = horiz(x);
+    u2 s3, c3;
+    s3.lo = lop3<kXor3>(hz.Le, x.lo, x.hi);
+    c3.lo = lop3<kMaj>(hz.Le, x.lo, x.hi);
+    s3.hi = lop3<kXor3>(x.lo, x.hi, hz.Ro);
+    c3.hi = lop3<kMaj>(x.lo, x.hi, hz.Ro);
     u2 y;
-    y.lo = rule32<RULE>(st.ps.lo, st.pc.lo, st.hs.lo, st.hc.lo, lop3<kXor3>(hz.Le, x.lo, x.hi),
-                        lop3<kMaj>(hz.Le, x.lo, x.hi), st.al.lo, birth, survive);
-    y.hi = rule32<RULE>(st.ps.hi, st.pc.hi, st.hs.hi, st.hc.hi, lop3<kXor3>(x.lo, x.hi, hz.Ro),
-                        lop3<kMaj>(x.lo, x.hi, hz.Ro), st.al.hi, birth, survive);
-    st.ps.lo = st.hs.lo ^ st.al.lo;
-    st.ps.hi = st.hs.hi ^ st.al.hi;
-    st.pc.lo = lop3<kOrAnd>(st.hc.lo, st.hs.lo, st.al.lo);
-    st.pc.hi = lop3<kOrAnd>(st.hc.hi, st.hs.hi, st.al.hi);
-    st.hs.lo = hz.Le ^ x.hi;
-    st.hs.hi = x.lo ^ hz.Ro;
-    st.hc.lo = hz.Le & x.hi;
-    st.hc.hi = x.lo & hz.Ro;
+    y.lo = rule32_total<RULE>(st.ps.lo, st.pc.lo, st.cs.lo, st.cc.lo, s3.lo, c3.lo, st.al.lo,
+                                  birth, survive);
+    y.hi = rule32_total<RULE>(st.ps.hi, st.pc.hi, st.cs.hi, st.cc.hi, s3.hi, c3.hi, st.al.hi,
+                                  birth, survive);
+    st.ps = st.cs;
+    st.pc = st.cc;
+    st.cs = s3;
+    st.cc = c3;
     st.al = x;
     return y;
 }
 
-template <bool COMPACT>
+// VAR: 0 = total-sum state, anti-diagonal schedule; 1 = neighbour-sum state,
+// anti-diagonal; 2 = as 0 with the plain step-major schedule.
+template <int RULE, int VAR>
 struct StageOf {
-    using type = Stage;
-};
-template <>
-struct StageOf<true> {
-    using type = StageC;
+    using type = typename std::conditional<VAR != 1, StageT, Stage>::type;
 };
 
 constexpr int kPrefetch = 4;
 
 
-// VAR: 0 = full state, 1 = compact state, 2 = full state with the plain
-// (step-major) schedule instead of the anti-diagonal one
 template <int K, int RULE, int VAR>
 __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 {
-    constexpr bool COMPACT = VAR == 1;
     constexpr bool kDiagonal = VAR != 2;
     constexpr bool kBirths = RULE != RULE_REF;
     const int lane = threadIdx.x & 63;
@@ -241,7 +320,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     const int64_t lo_ok = max((int64_t)0, -sg.glob0);             // first local row in field
     const int64_t hi_ok = min(sg.in_rows, sg.field_h - sg.glob0);  // one past last
 
-    typename StageOf<COMPACT>::type st[K];
+    typename StageOf<RULE, VAR>::type st[K];
 #pragma unroll
     for (int g = 0; g < K; ++g) st[g] = {};
 
@@ -323,20 +402,20 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     }
 }
 
-template <int K, int COMPACT>
+template <int K, int VAR>
 hipError_t launch_depth(const StepArgs& a, RuleKind rule, hipStream_t s)
 {
     const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
     const dim3 block(64 * kWavesPerBlock);
     switch (rule) {
     case RULE_REF:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, COMPACT>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, VAR>), grid, block, 0, s, a);
         break;
     case RULE_CONWAY:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, COMPACT>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, VAR>), grid, block, 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, COMPACT>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, VAR>), grid, block, 0, s, a);
         break;
     }
     return hipGetLastError();
@@ -346,13 +425,15 @@ template <int K>
 hipError_t launch_variant(const StepArgs& a, RuleKind rule, int var, hipStream_t s)
 {
     switch (var) {
-    case 1: return launch_depth<K, 1>(a, rule, s);
+    case 1:  // the neighbour-sum state exists up to depth 16 (14 VGPRs per stage)
+        if constexpr (K <= 16) return launch_depth<K, 1>(a, rule, s);
+        return hipErrorInvalidValue;
     case 2: return launch_depth<K, 2>(a, rule, s);
     default: return launch_depth<K, 0>(a, rule, s);
     }
 }
 
-template <int K, int COMPACT>
+template <int K, int VAR>
 int occupancy_of(RuleKind rule)
 {
     int blocks = 0;
@@ -360,13 +441,13 @@ int occupancy_of(RuleKind rule)
     const int threads = 64 * kWavesPerBlock;
     if (rule == RULE_REF)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_REF, COMPACT>, threads, 0);
+            &blocks, life_tb_kernel<K, RULE_REF, VAR>, threads, 0);
     else if (rule == RULE_CONWAY)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_CONWAY, COMPACT>, threads, 0);
+            &blocks, life_tb_kernel<K, RULE_CONWAY, VAR>, threads, 0);
     else
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_GENERIC, COMPACT>, threads, 0);
+            &blocks, life_tb_kernel<K, RULE_GENERIC, VAR>, threads, 0);
     return e == hipSuccess ? blocks : 0;
 }
 
@@ -374,7 +455,9 @@ template <int K>
 int occupancy_variant(RuleKind rule, int var)
 {
     switch (var) {
-    case 1: return occupancy_of<K, 1>(rule);
+    case 1:
+        if constexpr (K <= 16) return occupancy_of<K, 1>(rule);
+        return 0;
     case 2: return occupancy_of<K, 2>(rule);
     default: return occupancy_of<K, 0>(rule);
     }
@@ -489,6 +572,9 @@ hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int compact,
     case 8: return launch_variant<8>(a, rule, compact, s);
     case 12: return launch_variant<12>(a, rule, compact, s);
     case 16: return launch_variant<16>(a, rule, compact, s);
+    case 20: return launch_variant<20>(a, rule, compact, s);
+    case 24: return launch_variant<24>(a, rule, compact, s);
+    case 32: return launch_variant<32>(a, rule, compact, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -504,6 +590,9 @@ int life_blocks_per_cu(int depth, RuleKind rule, int compact)
     case 8: return occupancy_variant<8>(rule, compact);
     case 12: return occupancy_variant<12>(rule, compact);
     case 16: return occupancy_variant<16>(rule, compact);
+    case 20: return occupancy_variant<20>(rule, compact);
+    case 24: return occupancy_variant<24>(rule, compact);
+    case 32: return occupancy_variant<32>(rule, compact);
     default: return 0;
     }
 }

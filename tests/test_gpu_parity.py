@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 GOLD = json.load(open(os.path.join(GOLDEN, "ref_outputs.json")))
 H, W = GOLD["h"], GOLD["w"]
-DEPTHS = [1, 2, 4, 6, 7, 8, 12, 16]
+DEPTHS = [1, 2, 4, 6, 7, 8, 12, 16, 20, 24, 32]
 
 
 def mask(ns):
@@ -80,9 +80,9 @@ def test_random_fields_every_depth(pkg, oracle, shape, rule):
     seed = h * 1000 + w
     want = {}
     g = oracle.bp_random(h, w, seed)
-    for gens in (1, 3, 16, 21):
+    for gens in (1, 3, 16, 21, 70):
         want[gens] = oracle.bp_run(g, w, gens, R)
-    for depth, variant in [(d, v) for d in DEPTHS for v in (1, 2, 3)]:
+    for depth, variant in [(d, v) for d in DEPTHS for v in (1, 2, 3) if v != 2 or d <= 16]:
         for gens, ref in want.items():
             with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth,
                             kernel_variant=variant) as e:
@@ -207,7 +207,7 @@ def test_c3_65536_vs_oracle(pkg, oracle):
 @pytest.mark.slow
 def test_c3_65536_depths_agree(pkg):
     digests = set()
-    for depth in (1, 8, 16):
+    for depth in (1, 8, 16, 32):
         with pkg.Engine(65536, 65536, rule=(1 << 3, 12), device=0, tb_depth=depth) as e:
             e.init_random(2)
             e.step(48)

@@ -34,6 +34,24 @@ constexpr int kIters = 4096;
 #define ALIGN(i) "v_alignbit_b32 %" #i ", %" #i ", %16, 31\n"
 #define DPP(i) "v_mov_b32_dpp %" #i ", %" #i " wave_shr:1 row_mask:0xf bank_mask:0xf\n"
 #define ANDOR(i) "v_and_or_b32 %" #i ", %" #i ", %16, %17\n"
+#define ORDPP(i) "v_or_b32_dpp %" #i ", %" #i ", %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n"
+#define ROWDPP(i) "v_mov_b32_dpp %" #i ", %" #i " row_shr:1 row_mask:0xf bank_mask:0xf\n"
+#define LSHL(i) "v_lshlrev_b32 %" #i ", 1, %" #i "\n"
+#define LSHLOR(i) "v_lshl_or_b32 %" #i ", %" #i ", 1, %16\n"
+#define ADDC(i) "v_addc_co_u32 %" #i ", vcc, %" #i ", %" #i ", vcc\n"
+#define ADDC64(i) "v_addc_co_u32_e64 %" #i ", s[60:61], %" #i ", %" #i ", s[62:63]\n"
+#define CMPV(i) "v_cmp_gt_i32_e64 s[60:61], 0, %" #i "\n"
+#define ORROWDPP(i) "v_or_b32_dpp %" #i ", %" #i ", %16 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n"
+
+#define BODY16S(INSTR)                                                                     \
+    asm volatile(INSTR(0) INSTR(1) INSTR(2) INSTR(3) INSTR(4) INSTR(5) INSTR(6) INSTR(7)  \
+                     INSTR(8) INSTR(9) INSTR(10) INSTR(11) INSTR(12) INSTR(13) INSTR(14)  \
+                     INSTR(15)                                                             \
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), \
+                   "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), \
+                   "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15])                      \
+                 : "v"(k1), "v"(k2)                                                        \
+                 : "vcc", "s60", "s61", "s62", "s63")
 
 template <int OP>
 __global__ __launch_bounds__(256) void rate_kernel(unsigned* out, unsigned k1, unsigned k2)
@@ -48,6 +66,14 @@ __global__ __launch_bounds__(256) void rate_kernel(unsigned* out, unsigned k1, u
         if constexpr (OP == 3) BODY16(ALIGN);
         if constexpr (OP == 4) BODY16(DPP);
         if constexpr (OP == 5) BODY16(ANDOR);
+        if constexpr (OP == 6) BODY16(ORDPP);
+        if constexpr (OP == 7) BODY16(ROWDPP);
+        if constexpr (OP == 8) BODY16(LSHL);
+        if constexpr (OP == 9) BODY16(LSHLOR);
+        if constexpr (OP == 10) BODY16(ORROWDPP);
+        if constexpr (OP == 11) BODY16S(ADDC);
+        if constexpr (OP == 12) BODY16S(CMPV);
+        if constexpr (OP == 13) BODY16S(ADDC64);
     }
     unsigned acc = 0;
 #pragma unroll
@@ -83,12 +109,21 @@ int main()
     unsigned* d;
     CHK(hipMalloc(&d, sizeof(unsigned) * blocks * 256));
     const char* names[] = {"v_xor_b32", "v_bitop3_b32", "v_add3_u32", "v_alignbit_b32",
-                           "v_mov_b32_dpp", "v_and_or_b32"};
-    double r[6] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks),
-                   run<4>(d, blocks), run<5>(d, blocks)};
+                           "v_mov_b32_dpp", "v_and_or_b32", "v_or_b32_dpp_wave_shr",
+                           "v_mov_b32_dpp_row_shr", "v_lshlrev_b32", "v_lshl_or_b32",
+                           "v_or_b32_dpp_row_shr", "v_addc_co_u32", "v_cmp_gt_i32_e64",
+                           "v_addc_co_u32_e64"};
+    constexpr int N = 14;
+    double r[N] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks),
+                   run<4>(d, blocks), run<5>(d, blocks), run<6>(d, blocks), run<7>(d, blocks),
+                   run<8>(d, blocks), run<9>(d, blocks), run<10>(d, blocks),
+                   run<11>(d, blocks), run<12>(d, blocks), run<13>(d, blocks)};
     std::printf("{\"cus\": %d, \"clock_mhz_prop\": %d", cus, p.clockRate / 1000);
-    for (int i = 0; i < 6; ++i)
+    for (int i = 0; i < N; ++i)
         std::printf(", \"%s\": %.4g", names[i], r[i] / (4.0 * cus));  // per SIMD per second
+    // issue rate vs resident waves per SIMD (16 independent chains per wave)
+    std::printf(", \"v_bitop3_b32_1wave\": %.4g", run<1>(d, cus) / (4.0 * cus));
+    std::printf(", \"v_bitop3_b32_2waves\": %.4g", run<1>(d, 2 * cus) / (4.0 * cus));
     std::printf(", \"unit\": \"wave-instructions per SIMD per second\"}\n");
     return 0;
 }
