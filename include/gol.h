@@ -84,7 +84,10 @@ typedef struct gol_config {
                               the device (k-deep halos, device copies), so one
                               stripe's launch tail overlaps the others' work;
                               0 = auto (2 when h >= 32768), 1 = one stream */
-    uint32_t reserved[2];
+    uint32_t strip_lanes;  /* lanes per column strip of the stencil kernel: 64, 32
+                              or 16 (2 of them halo, 64/L strips per wavefront);
+                              0 = auto (narrow strips for short stripes) */
+    uint32_t reserved[1];
 } gol_config;
 
 typedef struct gol_engine gol_engine;
@@ -149,6 +152,10 @@ gol_status gol_reset_timing(gol_engine* e);
 gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0,
                     uint64_t* rows, uint32_t* tb_depth, uint32_t* halo_depth,
                     uint32_t* rows_per_wave);
+
+/* Launch plan of a full-depth launch as chosen (strip width in lanes, rows per
+ * wavefront); a composite engine reports its first stripe's plan. */
+gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave);
 
 /* ---- Multi-GPU, one process per GPU (replaces the MPI stripes :70-81 and the
  * halo exchange :104-145 with RCCL send/recv over xGMI) ---- */

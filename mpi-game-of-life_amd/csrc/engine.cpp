@@ -116,6 +116,7 @@ struct gol_engine {
     gol::RuleKind rule = gol::RULE_REF;
     uint32_t K = 8;
     uint32_t rows_per_wave = 0;
+    int lane_shift = -1;  // strip width 64 >> lane_shift; -1 = chosen per plan
     int var = 0;  // stencil kernel variant (life_internal.h launch_life)
     uint32_t sem = GOL_SEM_GLOBAL;
     uint32_t P = 1;
@@ -136,8 +137,11 @@ struct gol_engine {
     // launch; the exchange runs on `comm` between them.  plans[Hx] = band,
     // plans[Hx+1] = interior.  halo_fresh: the current buffer's halo rows were
     // already exchanged (completion signalled by ev_xdone on `comm`).
-    hipStream_t comm_stream = nullptr;
-    hipEvent_t ev_band = nullptr, ev_xdone = nullptr;
+    // The band launch runs on its own stream, concurrently with the interior
+    // launch: it is a few hundred rows, far too few wavefronts to fill the GPU,
+    // so serialising it before the interior would leave the chip mostly idle.
+    hipStream_t comm_stream = nullptr, band_stream = nullptr;
+    hipEvent_t ev_band = nullptr, ev_xdone = nullptr, ev_in = nullptr;
     bool overlap = false;
     bool halo_fresh = false;
 
@@ -154,13 +158,14 @@ struct gol_engine {
     // plans: plan p = a device table of nseg SegDesc (+ host copy)
     struct Plan {
         std::vector<SegDesc> segs;
+        int32_t groups = 0;      // strip groups per row block (StepArgs::strips)
+        int32_t lane_shift = 0;  // strips of 64 >> lane_shift lanes
         double own_rows = 0;  // output rows of this plan that are the caller's rows
         int64_t rpw = 0;      // rows per wavefront
         int64_t total_units = 0;
         SegDesc* dev = nullptr;
     };
     std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: plans[c-1] for shrink c
-    int32_t strips = 0;
 
     std::vector<Region> user_regions;  // load/store mapping (own output rows)
     std::vector<Region> load_regions;  // rows loaded (REF_STRIPES loads overlaps too)
@@ -202,39 +207,63 @@ void finish_segs(std::vector<SegDesc>& segs, int64_t rpw, int32_t strips)
     }
 }
 
-// Rows per wavefront for one launch plan.  Every wavefront of a launch does the
-// same work, (R + K + 1) stage-steps of K stages (R output rows, K+1 rows of
-// warm-up/halo), so the launch time is set by the most loaded SIMD:
-// n = ceil(units / SIMDs) wavefronts run in rounds of `occ` resident ones, and
-// a partial round of m wavefronts still costs max(2, m) issue slots per
+// Strip groups per row block for strips of 64 >> shift lanes.
+int32_t strip_groups(uint64_t wq, int shift)
+{
+    const uint64_t out = (uint64_t)((64 >> shift) - 2);
+    const uint64_t strips = (wq + out - 1) / out;
+    const uint64_t per = 1ull << shift;
+    return (int32_t)((strips + per - 1) / per);
+}
+
+// Rows per wavefront and strip width for one launch plan.  Every wavefront of
+// a launch does the same work, (R + K + 1) stage-steps of K stages (R output
+// rows, K+1 rows of warm-up/halo), so the launch time is set by the most loaded
+// SIMD: n = ceil(units / SIMDs) wavefronts run in rounds of `occ` resident ones,
+// and a partial round of m wavefronts still costs max(2, m) issue slots per
 // instruction (one wavefront alone issues at half the SIMD's VALU rate).
 // Measured (profiles/r01/sweep_rows_per_wave*.jsonl): keeping fewer than `occ`
 // wavefronts per SIMD all launch long is 5-10% slower than the model says, so
-// R is restricted to n >= occ whenever the field is large enough.
-int64_t pick_rows_per_wave(const std::vector<SegDesc>& segs, int32_t strips, int K, int occ,
-                           int simds)
+// R is restricted to n >= occ whenever the field is large enough.  Narrower
+// strips (32 or 16 lanes, 2 or 4 per wavefront) multiply the units per row
+// block, so short stripes reach `occ` with longer row blocks; the model picks
+// the cheapest (strip width, R).
+struct RowPlan {
+    int64_t rpw;
+    int32_t groups, lane_shift;
+};
+
+RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K, int occ,
+                           int simds, int force_rpw, int force_shift)
 {
     const int64_t c0 = 3;  // per-wavefront fixed cost, in rows
     int64_t maxrows = 1;
     for (const auto& s : segs) maxrows = std::max<int64_t>(maxrows, s.out_hi - s.out_lo);
-    int64_t best_r[2] = {16, 16};
+    RowPlan best_p[2] = {{16, strip_groups(wq, 0), 0}, {16, strip_groups(wq, 0), 0}};
     double best[2] = {1e300, 1e300};
-    for (int64_t R = std::max<int64_t>(8, K + 2); R <= std::min<int64_t>(1024, maxrows + K); ++R) {
-        int64_t units = 0;
-        for (const auto& sg : segs)
-            units += strips * ((std::max<int64_t>(0, sg.out_hi - sg.out_lo) + R - 1) / R);
-        const int64_t n = (units + simds - 1) / simds;
-        const int64_t full = n / occ, rem = n % occ;
-        const double slots =
-            (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
-        const double cost = slots * (double)(R + K + 1 + c0);
-        const int filled = n >= occ ? 1 : 0;
-        if (cost < best[filled] * 0.999) {
-            best[filled] = cost;
-            best_r[filled] = R;
+    for (int shift = 0; shift <= 2; ++shift) {
+        if (force_shift >= 0 && shift != force_shift) continue;
+        const int32_t groups = strip_groups(wq, shift);
+        const int64_t r_lo = force_rpw ? force_rpw : std::max<int64_t>(8, K + 2);
+        const int64_t r_hi =
+            force_rpw ? force_rpw : std::max<int64_t>(r_lo, std::min<int64_t>(1024, maxrows + K));
+        for (int64_t R = r_lo; R <= r_hi; ++R) {
+            int64_t units = 0;
+            for (const auto& sg : segs)
+                units += groups * ((std::max<int64_t>(0, sg.out_hi - sg.out_lo) + R - 1) / R);
+            const int64_t n = (units + simds - 1) / simds;
+            const int64_t full = n / occ, rem = n % occ;
+            const double slots =
+                (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
+            const double cost = slots * (double)(R + K + 1 + c0);
+            const int filled = n >= occ ? 1 : 0;
+            if (cost < best[filled] * 0.999) {
+                best[filled] = cost;
+                best_p[filled] = {R, groups, shift};
+            }
         }
     }
-    return best[1] < 1e300 ? best_r[1] : best_r[0];
+    return best[1] < 1e300 ? best_p[1] : best_p[0];
 }
 
 gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
@@ -245,10 +274,13 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     for (const auto& r : raw) {
         gol_engine::Plan p;
         p.segs = r;
-        p.rpw = e->rows_per_wave ? (int64_t)e->rows_per_wave
-                                 : pick_rows_per_wave(r, e->strips, (int)e->K, occ, 4 * cus);
-        finish_segs(p.segs, p.rpw, e->strips);
-        p.total_units = plan_units(p.segs, e->strips);
+        const RowPlan rp = pick_rows_per_wave(r, e->wq, (int)e->K, occ, 4 * cus,
+                                              (int)e->rows_per_wave, e->lane_shift);
+        p.rpw = rp.rpw;
+        p.groups = rp.groups;
+        p.lane_shift = rp.lane_shift;
+        finish_segs(p.segs, p.rpw, p.groups);
+        p.total_units = plan_units(p.segs, p.groups);
         for (const auto& sg : p.segs) {
             // own rows of a segment: rank engines [Hx, Hx+R); REF_STRIPES the
             // rank's output rows; GLOBAL all rows
@@ -283,6 +315,9 @@ gol_status check_cfg(const gol_config* cfg)
                                         (int)cfg->tb_depth) == std::end(gol::kDepthList))
         return fail(GOL_EINVAL, "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16,20,24,32");
     if (cfg->kernel_variant > 3) return fail(GOL_EINVAL, "kernel_variant must be 0..3");
+    if (cfg->strip_lanes != 0 && cfg->strip_lanes != 64 && cfg->strip_lanes != 32 &&
+        cfg->strip_lanes != 16)
+        return fail(GOL_EINVAL, "strip_lanes must be 0 (auto), 64, 32 or 16");
     if (cfg->kernel_variant == 2 && cfg->tb_depth > 16)
         return fail(GOL_EINVAL, "kernel_variant 2 (neighbour-sum state) needs tb_depth <= 16");
     if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
@@ -307,16 +342,19 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->rule = gol::RULE_GENERIC;
     e->K = cfg->tb_depth ? cfg->tb_depth : auto_depth(e->R, cfg);
     e->rows_per_wave = cfg->rows_per_wave;
+    e->lane_shift = cfg->strip_lanes == 64 ? 0 : cfg->strip_lanes == 32 ? 1
+                  : cfg->strip_lanes == 16 ? 2 : -1;
     e->var = cfg->kernel_variant == 2 ? 1 : cfg->kernel_variant == 3 ? 2 : 0;
     e->sem = cfg->semantics;
-    e->strips = (int32_t)((e->wq + gol::kStripOut - 1) / gol::kStripOut);
 
     if (cfg->device >= 0) HIP_TRY(hipSetDevice(cfg->device));
     HIP_TRY(hipGetDevice(&e->device));
     HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     if (e->nranks > 1) {
         HIP_TRY(hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&e->band_stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&e->ev_band, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&e->ev_xdone, hipEventDisableTiming));
     }
 
@@ -455,15 +493,18 @@ gol_status get_event(gol_engine* e, hipEvent_t* ev)
     return GOL_OK;
 }
 
-gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true)
+gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
+                  hipStream_t stream = nullptr)
 {
+    hipStream_t s = stream ? stream : e->stream;
     const auto& p = e->plans[plan];
     StepArgs a{};
     a.in = e->buf[e->cur];
     a.out = e->buf[e->cur ^ 1];
     a.segs = p.dev;
     a.nseg = (int32_t)p.segs.size();
-    a.strips = e->strips;
+    a.strips = p.groups;
+    a.lane_shift = p.lane_shift;
     a.stride = (int64_t)e->stride;
     a.wq = (int64_t)e->wq;
     a.lastmask = gol_split64(e->lastmask);  // the kernel works on column-split words
@@ -477,11 +518,11 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true)
         gol_status st = get_event(e, &e0);
         if (st == GOL_OK) st = get_event(e, &e1);
         if (st != GOL_OK) return st;
-        HIP_TRY(hipEventRecord(e0, e->stream));
+        HIP_TRY(hipEventRecord(e0, s));
     }
-    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->var, e->stream));
+    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->var, s));
     if (timed) {
-        HIP_TRY(hipEventRecord(e1, e->stream));
+        HIP_TRY(hipEventRecord(e1, s));
         e->ev_pending.push_back({e0, e1});
         double comp = 0;
         for (const auto& s : p.segs) comp += (double)(s.out_hi - s.out_lo);
@@ -730,11 +771,13 @@ void gol_destroy(gol_engine* e)
     }
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
+    if (e->band_stream) (void)hipStreamSynchronize(e->band_stream);
     // group neighbours may still be copying from this engine's buffers
     for (gol_engine* n : {e->up, e->down}) {
         if (!n) continue;
         if (n->stream) (void)hipStreamSynchronize(n->stream);
         if (n->comm_stream) (void)hipStreamSynchronize(n->comm_stream);
+        if (n->band_stream) (void)hipStreamSynchronize(n->band_stream);
     }
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->up) e->up->down = nullptr;
@@ -742,7 +785,10 @@ void gol_destroy(gol_engine* e)
     if (e->ev_ready) (void)hipEventDestroy(e->ev_ready);
     if (e->ev_copied) (void)hipEventDestroy(e->ev_copied);
     if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
+    if (e->band_stream) (void)hipStreamSynchronize(e->band_stream);
     if (e->ev_band) (void)hipEventDestroy(e->ev_band);
+    if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+    if (e->band_stream) (void)hipStreamDestroy(e->band_stream);
     if (e->ev_xdone) (void)hipEventDestroy(e->ev_xdone);
     if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
     for (auto& p : e->plans)
@@ -784,6 +830,7 @@ static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs, bool
 {
     HIP_TRY(hipSetDevice(e->device));
     if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
+    if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->halo_fresh = false;
     // clear everything (halos, unused rows) then copy each region, masking pad bits
@@ -877,6 +924,7 @@ gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
     // raw bytes to the device, packed there by the ASCII codec kernel
     HIP_TRY(hipSetDevice(e->device));
     if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
+    if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->halo_fresh = false;
     DeviceBytes bytes;
@@ -960,6 +1008,7 @@ gol_status gol_init_random(gol_engine* e, uint64_t seed)
     }
     HIP_TRY(hipSetDevice(e->device));
     if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
+    if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->halo_fresh = false;
     const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
@@ -993,9 +1042,12 @@ gol_status run_round(gol_engine* e, uint64_t round, Xchg&& xchg)
         done += d;
         gol_status st;
         if (e->overlap && done == e->Hx) {
-            st = launch(e, (int)e->Hx, d, false);  // band rows first
+            // band rows on the band stream, concurrent with the interior launch
+            HIP_TRY(hipEventRecord(e->ev_in, e->stream));
+            HIP_TRY(hipStreamWaitEvent(e->band_stream, e->ev_in, 0));
+            st = launch(e, (int)e->Hx, d, false, e->band_stream);
             if (st != GOL_OK) return st;
-            HIP_TRY(hipEventRecord(e->ev_band, e->stream));
+            HIP_TRY(hipEventRecord(e->ev_band, e->band_stream));
             st = launch(e, (int)e->Hx + 1, d, false);  // interior, overlaps the exchange
             if (st != GOL_OK) return st;
             e->cur ^= 1;
@@ -1204,6 +1256,7 @@ gol_status gol_sync(gol_engine* e)
         return GOL_OK;
     }
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
     if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
     return GOL_OK;
 }
@@ -1316,6 +1369,18 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uin
     if (rows) *rows = e->nranks > 1 ? e->R : e->H;
     if (tb_depth) *tb_depth = e->K;
     if (halo_depth) *halo_depth = (uint32_t)e->Hx;
+    return GOL_OK;
+}
+
+gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) return gol_plan_info(e->parts[0], strip_lanes, rows_per_wave);
+    if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
+    // rank engines: plans[Hx-1] is the full-round launch over own rows; else plans[0]
+    const auto& p = e->nranks > 1 ? e->plans[e->Hx - 1] : e->plans[0];
+    if (strip_lanes) *strip_lanes = (uint32_t)(64 >> p.lane_shift);
+    if (rows_per_wave) *rows_per_wave = (uint32_t)p.rpw;
     return GOL_OK;
 }
 

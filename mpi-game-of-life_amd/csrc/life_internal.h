@@ -29,9 +29,13 @@ struct SegDesc {
     int64_t unit0;  // index of this segment's first wavefront in the launch
 };
 
-// Output words per wavefront strip: 64 lanes each hold one 64-bit word; lanes 0
-// and 63 are the horizontal halo (valid up to 63 fused generations).
-constexpr int kStripOut = 62;
+// Strips: a strip is L consecutive lanes (L = 64 >> lane_shift: 64, 32 or 16),
+// each holding one 64-bit word of a row; its first and last lane are the
+// horizontal halo (exact for up to 63 fused generations), so a strip outputs
+// L - 2 words.  A wavefront runs 64 / L strips side by side over the same rows:
+// narrow strips trade 2 halo lanes per strip for more wavefronts per row block,
+// which lets short stripes use longer row blocks (less vertical halo recompute).
+constexpr int kStripOut = 62;  // output words of a full 64-lane strip
 constexpr int kWavesPerBlock = 4;
 // Zeroed guard rows allocated before/after every state buffer so that the
 // streaming loads (K rows of halo + prefetch distance) never leave the allocation.
@@ -43,7 +47,8 @@ struct StepArgs {
     uint64_t* out;
     const SegDesc* segs;  // device table
     int32_t nseg;
-    int32_t strips;       // ceil(wq / kStripOut)
+    int32_t strips;       // strip groups per row: ceil(ceil(wq / (L-2)) / (64/L))
+    int32_t lane_shift;   // L = 64 >> lane_shift lanes per strip (0, 1 or 2)
     int64_t stride;       // words per buffer row
     int64_t wq;           // words per field row = ceil(w / 64)
     uint64_t lastmask;    // valid bits of word wq-1

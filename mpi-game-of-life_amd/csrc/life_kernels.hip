@@ -33,7 +33,14 @@
 
 #include "bitlayout.h"
 #include "life_internal.h"
+#include "loop_place.h"
 
+#ifndef GOL_WARM_ROLLED
+#define GOL_WARM_ROLLED 0
+#endif
+#ifndef GOL_HORIZ_BPERM
+#define GOL_HORIZ_BPERM 0
+#endif
 #ifndef GOL_HORIZ_ADDC
 #define GOL_HORIZ_ADDC 0
 #endif
@@ -128,7 +135,21 @@ struct Horiz {
 };
 __device__ __forceinline__ Horiz horiz(u2 x)
 {
-#if GOL_HORIZ_ADDC
+#if GOL_HORIZ_BPERM
+    // neighbour lanes through the LDS crossbar (ds_bpermute) instead of DPP moves,
+    // which issue on the VALU at half rate; byte address of lane l-1 / l+1
+    const int lane4 = (int)__lane_id() * 4;
+    const uint32_t hp = (uint32_t)__builtin_amdgcn_ds_bpermute(lane4 - 4, (int)x.hi);
+#if GOL_HORIZ_BPERM == 2  // one direction each way: LDS crossbar and DPP
+    const uint32_t ln = lane_from_right(x.lo);
+#else
+    const uint32_t ln = (uint32_t)__builtin_amdgcn_ds_bpermute(lane4 + 4, (int)x.lo);
+#endif
+    Horiz h;
+    h.Le = __builtin_amdgcn_alignbit(x.hi, hp, 31);
+    h.Ro = __builtin_amdgcn_alignbit(ln, x.lo, 1);
+    return h;
+#elif GOL_HORIZ_ADDC
     // left shift with the carry from lane l-1 as an add-with-carry: the carries of
     // all lanes are one wave mask (v_cmp), moved up one lane on the scalar unit
     const uint64_t m = __builtin_amdgcn_ballot_w64((int32_t)x.hi < 0) << 1;
@@ -209,7 +230,8 @@ struct StageT {
 };
 constexpr uint32_t kAnd3 = 0x80;     // a & b & c
 constexpr uint32_t kFour = 0x42;     // ~(a ^ b) & (a ^ c)
-constexpr uint32_t kMux = 0xCA;      // a ? b : c
+constexpr uint32_t kAndNot = 0x40;   // a & b & ~c
+constexpr uint32_t kOrAnd2 = 0xEA;   // (a & b) | c
 
 template <int RULE>
 __device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint32_t bs,
@@ -228,9 +250,11 @@ __device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint3
         // Parallel_Life_MPI.cpp:47-50: alive && n == 2  <=>  alive && T == 3
         return lop3<kAnd3>(alive, s0, three);
     } else if constexpr (RULE == RULE_CONWAY) {
-        // T == 4  <=>  !s0 && (p + k0 == 2 && !mj  ||  p + k0 == 0 && mj)
-        const uint32_t four = lop3<kFour>(p, k0, mj) & alive;
-        return lop3<kMux>(s0, three, four);
+        // T == 4  <=>  !s0 && (p + k0 == 2 && !mj  ||  p + k0 == 0 && mj); all
+        // three steps are v_bitop3 (8-byte encodings, see loop_pad.h)
+        const uint32_t four = lop3<kFour>(p, k0, mj);
+        const uint32_t stay = lop3<kAndNot>(alive, four, s0);  // alive & four & !s0
+        return lop3<kOrAnd2>(s0, three, stay);                 // (s0 & three) | stay
     } else {
         // T = s0 + 2*x + 4*t2 + 8*t3; alive cells have n = T - 1, dead ones n = T
         const uint32_t x = p ^ k0, y = p & k0;
@@ -298,10 +322,20 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         if (unit >= a.segs[j].unit0) sidx = j;
     const SegDesc sg = a.segs[sidx];
     const int64_t u = unit - sg.unit0;
-    const int strip = (int)(u % a.strips);
     const int64_t blk = u / a.strips;
+    // strip `strip` of the row block lives in lanes [sub*L, sub*L + L); the DPP
+    // shifts cross from one strip into the next only at halo lanes
+#ifdef GOL_DEV_FULL_STRIPS
+    constexpr int L = 64, lshift = 0;
+#else
+    const int lshift = a.lane_shift;
+    const int L = 64 >> lshift;
+#endif
+    const int sub = lane >> (6 - lshift);
+    const int lin = lane & (L - 1);
+    const int strip = (int)(u % a.strips) * (1 << lshift) + sub;
 
-    const int64_t q = (int64_t)strip * kStripOut - 1 + lane;
+    const int64_t q = (int64_t)strip * (L - 2) - 1 + lin;
     const bool qin = (q >= 0) && (q < a.wq);
     const uint64_t cm = qin ? ((q == a.wq - 1) ? a.lastmask : ~0ull) : 0ull;
     const uint32_t cmlo = (uint32_t)cm, cmhi = (uint32_t)(cm >> 32);
@@ -314,7 +348,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 
     const uint64_t* inp = a.in + (sg.base_row + row_first) * a.stride + qc;
     uint64_t* outp = a.out + (sg.base_row + rb) * a.stride + qc;
-    const bool st_lane = qin && lane >= 1 && lane <= kStripOut;
+    const bool st_lane = qin && lin >= 1 && lin <= L - 2;
 
     // field-row validity of local row i (dead border) and buffer-row validity
     const int64_t lo_ok = max((int64_t)0, -sg.glob0);             // first local row in field
@@ -354,29 +388,50 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
             outp[(t - 2 * K) * a.stride] = ((uint64_t)x.hi << 32) | x.lo;
     };
 
-    // Warm-up, fully unrolled: stage g first emits a row that can reach a valid
-    // output at step 2g+2 and needs the two ingests before it, so it runs from
-    // step 2g on; skipping it earlier saves K*(K-1) of the 2K*K warm-up stage steps.
-    constexpr int kWarm = (2 * K + kPrefetch - 1) / kPrefetch * kPrefetch;
-#pragma unroll
-    for (int t = 0; t < kWarm; ++t) {
-        const int p = t % kPrefetch;
-        u2 x = ingest(t, ring[p]);
-        ring[p] = *pf;
-        pf += a.stride;
-#pragma unroll
-        for (int g = 0; g < K; ++g)
-            if (t >= 2 * g) x = stage(g, t, x);
-        if (t >= 2 * K) store(t, x);
-    }
-
-    for (int64_t t0 = kWarm; t0 < T; t0 += kPrefetch) {
+    // One block of kPrefetch steps.  GUARD (warm-up blocks): stage g first emits a
+    // row that can reach a valid output at step 2g+2 and needs the two ingests
+    // before it, so it only runs from step 2g on; skipping it earlier saves
+    // K*(K-1) of the 2K*K warm-up stage-steps.  The guard is wave-uniform (a
+    // scalar branch per stage-step).
+    auto block = [&](int64_t t0, auto guard) {
+        constexpr bool kGuard = decltype(guard)::value;
         u2 x[kPrefetch];
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
             x[p] = ingest(t0 + p, ring[p]);
             ring[p] = *pf;
             pf += a.stride;
+        }
+        // Code placement (steady-state blocks).  gfx950 issues this kernel's
+        // instruction mix (DPP move, v_alignbit, v_bitop3 chains; all 8-byte
+        // encodings) 10-25% faster when those instructions sit at addresses =
+        // 4 mod 8 with 2+ waves per SIMD, and faster at 0 mod 8 with one
+        // (tools/valu_rate.hip "mix_at_*"; in the kernel: identical code and
+        // registers, 89.6 vs 79.9 TCUPS, profiles/r01/loop_alignment_ab.jsonl).
+        // The scheduling barriers keep the 4-byte encodings (loads, ingest masks,
+        // SALU, stores) out of the compute, so one alignment directive places
+        // all of it.
+        if constexpr (!kGuard) {
+            // the block's inputs pass through the directive, so the compute that
+            // depends on them cannot be scheduled above it; "memory" keeps the
+            // loads above and the stores below.  The compiler may add a hazard
+            // s_nop after it, so the 4-byte pad that gives the wanted parity is
+            // per kernel: loop_place.h, generated by tools/loop_align.py.
+            static_assert(kPrefetch == 4, "placement asm names 4 inputs");
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (life_loop_pad(K, RULE, VAR))
+                asm volatile(".p2align 3\n\ts_nop 0"
+                             : "+v"(x[0].lo), "+v"(x[0].hi), "+v"(x[1].lo), "+v"(x[1].hi),
+                               "+v"(x[2].lo), "+v"(x[2].hi), "+v"(x[3].lo), "+v"(x[3].hi)
+                             :
+                             : "memory");
+            else
+                asm volatile(".p2align 3"
+                             : "+v"(x[0].lo), "+v"(x[0].hi), "+v"(x[1].lo), "+v"(x[1].hi),
+                               "+v"(x[2].lo), "+v"(x[2].hi), "+v"(x[3].lo), "+v"(x[3].hi)
+                             :
+                             : "memory");
+            __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (kDiagonal) {
             // stage g of step p only needs stage g-1 of step p and stage g of step
@@ -387,19 +442,34 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 #pragma unroll
                 for (int p = 0; p < kPrefetch; ++p) {
                     const int g = d - p;
-                    if (g >= 0 && g < K) x[p] = stage(g, t0 + p, x[p]);
+                    if (g >= 0 && g < K && (!kGuard || t0 + p >= 2 * g))
+                        x[p] = stage(g, t0 + p, x[p]);
                 }
             }
         } else {
 #pragma unroll
             for (int p = 0; p < kPrefetch; ++p) {
 #pragma unroll
-                for (int g = 0; g < K; ++g) x[p] = stage(g, t0 + p, x[p]);
+                for (int g = 0; g < K; ++g)
+                    if (!kGuard || t0 + p >= 2 * g) x[p] = stage(g, t0 + p, x[p]);
             }
         }
+        if constexpr (!kGuard) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) store(t0 + p, x[p]);
-    }
+    };
+
+    // Warm-up blocks as a rolled loop: unrolled, they would be ~4x the code of
+    // the steady-state body and push the kernel past the instruction cache.
+    constexpr int kWarm = (2 * K + kPrefetch - 1) / kPrefetch * kPrefetch;
+#if GOL_WARM_ROLLED
+#pragma clang loop unroll(disable)
+    for (int64_t t0 = 0; t0 < kWarm; t0 += kPrefetch) block(t0, std::true_type{});
+#else
+#pragma unroll
+    for (int t0 = 0; t0 < kWarm; t0 += kPrefetch) block(t0, std::true_type{});
+#endif
+    for (int64_t t0 = kWarm; t0 < T; t0 += kPrefetch) block(t0, std::false_type{});
 }
 
 template <int K, int VAR>
@@ -563,6 +633,10 @@ __global__ __launch_bounds__(256) void ascii_unpack_kernel(const uint64_t* src, 
 hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int compact, hipStream_t s)
 {
     if (a.total_units <= 0) return hipSuccess;
+#ifdef GOL_DEV_ONLY_DEPTH  // dev A/B builds: one depth only (fast compile)
+    if (depth != GOL_DEV_ONLY_DEPTH) return hipErrorInvalidValue;
+    return launch_variant<GOL_DEV_ONLY_DEPTH>(a, rule, compact, s);
+#else
     switch (depth) {
     case 1: return launch_variant<1>(a, rule, compact, s);
     case 2: return launch_variant<2>(a, rule, compact, s);
@@ -577,10 +651,14 @@ hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int compact,
     case 32: return launch_variant<32>(a, rule, compact, s);
     default: return hipErrorInvalidValue;
     }
+#endif
 }
 
 int life_blocks_per_cu(int depth, RuleKind rule, int compact)
 {
+#ifdef GOL_DEV_ONLY_DEPTH
+    return depth == GOL_DEV_ONLY_DEPTH ? occupancy_variant<GOL_DEV_ONLY_DEPTH>(rule, compact) : 0;
+#else
     switch (depth) {
     case 1: return occupancy_variant<1>(rule, compact);
     case 2: return occupancy_variant<2>(rule, compact);
@@ -595,6 +673,7 @@ int life_blocks_per_cu(int depth, RuleKind rule, int compact)
     case 32: return occupancy_variant<32>(rule, compact);
     default: return 0;
     }
+#endif
 }
 
 hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_t lastmask,

@@ -93,6 +93,25 @@ def test_random_fields_every_depth(pkg, oracle, shape, rule):
                 assert e.digest() == oracle.bp_digest(ref, w)
 
 
+@pytest.mark.parametrize("lanes", [64, 32, 16])
+@pytest.mark.parametrize("rule", ["ref", "conway", "daynight"])
+def test_strip_widths(pkg, oracle, lanes, rule):
+    """Narrow strips (32/16 lanes, 2/4 per wavefront): strip seams inside a
+    wavefront, partial last strip groups, every depth class."""
+    R = rules(oracle)[rule]
+    for h, w in [(1, 1), (7, 65), (40, 1921), (33, 1983), (129, 4097), (64, 900)]:
+        seed = 7 * h + w
+        g = oracle.bp_random(h, w, seed)
+        for depth in (1, 4, 16, 32):
+            for gens in (3, 33, 70):
+                ref = oracle.bp_run(g, w, gens, R)
+                with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth, strip_lanes=lanes) as e:
+                    assert e.strip_lanes == lanes
+                    e.init_random(seed)
+                    e.step(gens)
+                    assert (e.store_packed() == ref).all(), f"{h}x{w} depth {depth} gens {gens}"
+
+
 @pytest.mark.parametrize("rpw", [16, 32, 48, 100])
 @pytest.mark.parametrize("variant", [1, 2, 3])
 def test_row_blocking(pkg, oracle, rpw, variant):
@@ -100,11 +119,12 @@ def test_row_blocking(pkg, oracle, rpw, variant):
     h, w = 300, 4100
     g = oracle.bp_random(h, w, 5)
     ref = oracle.bp_run(g, w, 16, oracle.CONWAY)
-    with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw,
-                    kernel_variant=variant) as e:
-        e.init_random(5)
-        e.step(16)
-        assert (e.store_packed() == ref).all()
+    for lanes in (64, 32, 16):
+        with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw,
+                        kernel_variant=variant, strip_lanes=lanes) as e:
+            e.init_random(5)
+            e.step(16)
+            assert (e.store_packed() == ref).all(), lanes
 
 
 def test_load_packed_roundtrip(pkg, oracle):

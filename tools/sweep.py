@@ -23,6 +23,7 @@ def main():
     p.add_argument("--depths", default="4,8,16")
     p.add_argument("--rpw", default="0")
     p.add_argument("--variants", default="0")
+    p.add_argument("--lanes", default="0", help="strip widths (gol_config.strip_lanes)")
     p.add_argument("--streams", type=int, default=0, help="gol_config.streams (0 = auto)")
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--rule", default="ref")
@@ -34,15 +35,16 @@ def main():
     w = a.width or a.size
     variants = list(itertools.product([int(x) for x in a.depths.split(",")],
                                       [int(x) for x in a.rpw.split(",")],
-                                      [int(x) for x in a.variants.split(",")]))
+                                      [int(x) for x in a.variants.split(",")],
+                                      [int(x) for x in a.lanes.split(",")]))
     engines = {}
-    for d, r, kv in variants:
+    for d, r, kv, sl in variants:
         e = pkg.Engine(h, w, rule=rule, device=0, tb_depth=d, rows_per_wave=r,
-                       kernel_variant=kv, streams=a.streams)
+                       kernel_variant=kv, streams=a.streams, strip_lanes=sl)
         e.init_random(1)
         e.step(d)  # warm
         e.sync()
-        engines[(d, r, kv)] = e
+        engines[(d, r, kv, sl)] = e
         if len(engines) > 6:  # bound HBM use: 1 GiB per engine at 65536^2
             pass
     res = {v: [] for v in variants}
@@ -63,7 +65,7 @@ def main():
         r = sorted(res[v])
         med = r[len(r) // 2]
         print(json.dumps({"tb_depth": v[0], "rows_per_wave": v[1] or f"auto({engines[v].rows_per_wave})",
-                          "variant": v[2],
+                          "variant": v[2], "strip_lanes": engines[v].strip_lanes,
                           "gcups_wall_median": round(med[0], 1),
                           "gcups_wall_best": round(r[-1][0], 1),
                           "kernel_ms_avg": round(med[1], 4),

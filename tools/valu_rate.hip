@@ -43,6 +43,53 @@ constexpr int kIters = 4096;
 #define CMPV(i) "v_cmp_gt_i32_e64 s[60:61], 0, %" #i "\n"
 #define ORROWDPP(i) "v_or_b32_dpp %" #i ", %" #i ", %16 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n"
 
+#define BODY16A(PRE, INSTR)                                                                \
+    asm volatile(PRE INSTR(0) INSTR(1) INSTR(2) INSTR(3) INSTR(4) INSTR(5) INSTR(6) INSTR(7) \
+                     INSTR(8) INSTR(9) INSTR(10) INSTR(11) INSTR(12) INSTR(13) INSTR(14)  \
+                     INSTR(15)                                                             \
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), \
+                   "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), \
+                   "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15])                      \
+                 : "v"(k1), "v"(k2))
+#define BITOP3X(i) "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n" \
+                   "v_bitop3_b32 %" #i ", %" #i ", %17, %16 bitop3:0xe8\n"
+
+// a stage-like mix per chain: DPP move, funnel shift, 6 x bitop3 (8-byte encodings)
+#define MIX(i) "v_mov_b32_dpp %" #i ", %" #i " wave_shr:1 row_mask:0xf bank_mask:0xf\n" \
+               "v_alignbit_b32 %" #i ", %" #i ", %16, 31\n"                             \
+               "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n"                  \
+               "v_bitop3_b32 %" #i ", %" #i ", %17, %16 bitop3:0xe8\n"                  \
+               "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n"                  \
+               "v_bitop3_b32 %" #i ", %" #i ", %17, %16 bitop3:0xe8\n"                  \
+               "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n"                  \
+               "v_bitop3_b32 %" #i ", %" #i ", %17, %16 bitop3:0xe8\n"
+// interleaved chains: instruction k of chain i, then of chain i+1 (like the
+// compiler's schedule of independent stage-steps)
+#define MIX2(i, j) "v_mov_b32_dpp %" #i ", %" #i " wave_shr:1 row_mask:0xf bank_mask:0xf\n" \
+               "v_mov_b32_dpp %" #j ", %" #j " wave_shr:1 row_mask:0xf bank_mask:0xf\n"      \
+               "v_alignbit_b32 %" #i ", %" #i ", %16, 31\n"                             \
+               "v_alignbit_b32 %" #j ", %" #j ", %16, 31\n"                             \
+               "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n"                  \
+               "v_bitop3_b32 %" #j ", %" #j ", %16, %17 bitop3:0x96\n"                  \
+               "v_bitop3_b32 %" #i ", %" #i ", %17, %16 bitop3:0xe8\n"                  \
+               "v_bitop3_b32 %" #j ", %" #j ", %17, %16 bitop3:0xe8\n"                  \
+               "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n"                  \
+               "v_bitop3_b32 %" #j ", %" #j ", %16, %17 bitop3:0x96\n"                  \
+               "v_bitop3_b32 %" #i ", %" #i ", %17, %16 bitop3:0xe8\n"                  \
+               "v_bitop3_b32 %" #j ", %" #j ", %17, %16 bitop3:0xe8\n"
+#define BODY8PAIRS(PRE)                                                                     \
+    asm volatile(PRE MIX2(0, 1) MIX2(2, 3) MIX2(4, 5) MIX2(6, 7) MIX2(8, 9) MIX2(10, 11)      \
+                 MIX2(12, 13) MIX2(14, 15)                                                   \
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), \
+                   "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), \
+                   "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15])                      \
+                 : "v"(k1), "v"(k2))
+
+#define DPPX(i) "v_mov_b32_dpp %" #i ", %" #i " wave_shr:1 row_mask:0xf bank_mask:0xf\n"
+#define ALGX(i) "v_alignbit_b32 %" #i ", %" #i ", %16, 31\n"
+#define DB(i) DPPX(i) "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n"
+#define AB(i) ALGX(i) "v_bitop3_b32 %" #i ", %" #i ", %16, %17 bitop3:0x96\n"
+
 #define BODY16S(INSTR)                                                                     \
     asm volatile(INSTR(0) INSTR(1) INSTR(2) INSTR(3) INSTR(4) INSTR(5) INSTR(6) INSTR(7)  \
                      INSTR(8) INSTR(9) INSTR(10) INSTR(11) INSTR(12) INSTR(13) INSTR(14)  \
@@ -74,6 +121,20 @@ __global__ __launch_bounds__(256) void rate_kernel(unsigned* out, unsigned k1, u
         if constexpr (OP == 11) BODY16S(ADDC);
         if constexpr (OP == 12) BODY16S(CMPV);
         if constexpr (OP == 13) BODY16S(ADDC64);
+        if constexpr (OP == 14) BODY16A(".p2align 3\n", BITOP3X);
+        if constexpr (OP == 15) BODY16A(".p2align 3\ns_nop 0\n", BITOP3X);
+        if constexpr (OP == 16) BODY16A(".p2align 3\n", MIX);
+        if constexpr (OP == 17) BODY16A(".p2align 3\ns_nop 0\n", MIX);
+        if constexpr (OP == 18) BODY8PAIRS(".p2align 3\n");
+        if constexpr (OP == 19) BODY8PAIRS(".p2align 3\ns_nop 0\n");
+        if constexpr (OP == 20) BODY16A(".p2align 3\n", DPPX);
+        if constexpr (OP == 21) BODY16A(".p2align 3\ns_nop 0\n", DPPX);
+        if constexpr (OP == 22) BODY16A(".p2align 3\n", ALGX);
+        if constexpr (OP == 23) BODY16A(".p2align 3\ns_nop 0\n", ALGX);
+        if constexpr (OP == 24) BODY16A(".p2align 3\n", DB);
+        if constexpr (OP == 25) BODY16A(".p2align 3\ns_nop 0\n", DB);
+        if constexpr (OP == 26) BODY16A(".p2align 3\n", AB);
+        if constexpr (OP == 27) BODY16A(".p2align 3\ns_nop 0\n", AB);
     }
     unsigned acc = 0;
 #pragma unroll
@@ -122,6 +183,28 @@ int main()
     for (int i = 0; i < N; ++i)
         std::printf(", \"%s\": %.4g", names[i], r[i] / (4.0 * cus));  // per SIMD per second
     // issue rate vs resident waves per SIMD (16 independent chains per wave)
+    // the same 32 v_bitop3 (8-byte encodings) starting at 0 mod 8 vs 4 mod 8
+    std::printf(", \"v_bitop3_b32_at_0mod8\": %.4g", 2 * run<14>(d, blocks) / (4.0 * cus));
+    std::printf(", \"v_bitop3_b32_at_4mod8\": %.4g", 2 * run<15>(d, blocks) / (4.0 * cus));
+    std::printf(", \"v_bitop3_b32_at_0mod8_2waves\": %.4g", 2 * run<14>(d, 2 * cus) / (4.0 * cus));
+    std::printf(", \"v_bitop3_b32_at_4mod8_2waves\": %.4g", 2 * run<15>(d, 2 * cus) / (4.0 * cus));
+    {
+        const char* nm[] = {"dpp", "alignbit", "dpp+bitop3", "alignbit+bitop3"};
+        const int per[] = {1, 1, 2, 2};
+        double v[8] = {run<20>(d, 2 * cus), run<21>(d, 2 * cus), run<22>(d, 2 * cus),
+                       run<23>(d, 2 * cus), run<24>(d, 2 * cus), run<25>(d, 2 * cus),
+                       run<26>(d, 2 * cus), run<27>(d, 2 * cus)};
+        for (int i = 0; i < 4; ++i)
+            std::printf(", \"%s_at_0mod8_2w\": %.4g, \"%s_at_4mod8_2w\": %.4g", nm[i],
+                        per[i] * v[2 * i] / (4.0 * cus), nm[i], per[i] * v[2 * i + 1] / (4.0 * cus));
+    }
+    // stage-like mix (8 instructions per chain: 1 DPP, 1 alignbit, 6 bitop3)
+    for (int w = 1; w <= 4; w *= 2) {
+        std::printf(", \"mix_at_0mod8_%dw\": %.4g", w, 8 * run<16>(d, w * cus) / (4.0 * cus));
+        std::printf(", \"mix_at_4mod8_%dw\": %.4g", w, 8 * run<17>(d, w * cus) / (4.0 * cus));
+        std::printf(", \"mixpairs_at_0mod8_%dw\": %.4g", w, 6 * run<18>(d, w * cus) / (4.0 * cus));
+        std::printf(", \"mixpairs_at_4mod8_%dw\": %.4g", w, 6 * run<19>(d, w * cus) / (4.0 * cus));
+    }
     std::printf(", \"v_bitop3_b32_1wave\": %.4g", run<1>(d, cus) / (4.0 * cus));
     std::printf(", \"v_bitop3_b32_2waves\": %.4g", run<1>(d, 2 * cus) / (4.0 * cus));
     std::printf(", \"unit\": \"wave-instructions per SIMD per second\"}\n");
