@@ -57,7 +57,7 @@ def cpu_baseline(threads, w):
     """Oracle port of the reference algorithm, bounded sample: `threads` stripes of
     512 rows x w columns (like mpirun -np threads), 16 generations."""
     orc = entry.load_oracle()
-    rows, gens = 512, 16
+    rows, gens = 512, 64
     t0 = time.perf_counter()
     orc.ref_baseline(rows, w, 0, threads)
     t_init = time.perf_counter() - t0
