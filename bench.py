@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--size", type=int, default=65536, help="field is size x size")
     p.add_argument("--gens", type=int, default=1000, help="generations per step")
     p.add_argument("--tb-depth", type=int, default=0)
+    p.add_argument("--word-planes", type=int, default=0)
     p.add_argument("--rows-per-wave", type=int, default=0)
     p.add_argument("--halo-depth", type=int, default=0)
     p.add_argument("--rule", default="ref", choices=["ref", "conway"])
@@ -86,8 +87,9 @@ def traffic_for(cfg):
     except Exception:
         return None
     for r in rec.get("records", []):
-        if all(r.get(k, 1) == cfg.get(k) for k in ("size", "tb_depth", "rows_per_wave", "n_gpus",
-                                                    "streams")):
+        defaults = {"word_planes": 2}
+        if all(r.get(k, defaults.get(k, 1)) == cfg.get(k)
+               for k in ("size", "tb_depth", "rows_per_wave", "n_gpus", "streams", "word_planes")):
             return r.get("hbm_bytes_per_launch")
     return None
 
@@ -114,10 +116,11 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         eng = pkg.Engine(n, n, rule=rule, device=local, tb_depth=a.tb_depth,
                          rows_per_wave=a.rows_per_wave, halo_depth=a.halo_depth,
+                         word_planes=a.word_planes,
                          rank=rank, nranks=world, uid=uid[0])
     else:
         eng = pkg.Engine(n, n, rule=rule, device=local, tb_depth=a.tb_depth,
-                         rows_per_wave=a.rows_per_wave)
+                         rows_per_wave=a.rows_per_wave, word_planes=a.word_planes)
     eng.init_random(a.seed)
 
     def barrier():
@@ -162,7 +165,7 @@ def main():
     streams = max(1, tm.get("streams", 1))
     achieved = BYTES_PER_CELL_GEN * cg_per_launch * streams / (avg_launch_ms / 1e3) / 1e9
     cfg_key = {"size": n, "tb_depth": eng.tb_depth, "rows_per_wave": a.rows_per_wave,
-               "n_gpus": world, "streams": streams}
+               "n_gpus": world, "streams": streams, "word_planes": eng.word_planes}
     traffic = traffic_for(cfg_key)
 
     if rank == 0:
@@ -183,7 +186,8 @@ def main():
                 "workload": f"{n}x{n} bit-packed random grid, {a.gens} generations per step",
                 "h": n, "w": n, "gens_per_step": a.gens,
                 "rule": "B/S2 (reference effective rule)" if a.rule == "ref" else "B3/S23",
-                "tb_depth": eng.tb_depth, "halo_depth": eng.halo_depth,
+                "tb_depth": eng.tb_depth, "word_planes": eng.word_planes,
+                "halo_depth": eng.halo_depth,
                 "rows_per_wave": eng.rows_per_wave,
                 "parallelism": f"row-stripes x{world}" if world > 1 else "single GPU",
             },

@@ -75,9 +75,10 @@ typedef struct gol_config {
     uint32_t rows_per_wave;/* rows each wavefront streams per launch; 0 = auto */
     uint32_t kernel_variant;/* stencil kernel: 0 = auto (= 1); 1 = total-sum
                               state (9-cell sums, 10 VGPRs per fused
-                              generation), anti-diagonal schedule; 2 =
-                              neighbour-sum state (14 VGPRs, +4 VALU ops per
-                              word-generation, tb_depth <= 16); 3 = as 1 with a
+                              generation and plane pair), anti-diagonal
+                              schedule; 2 = neighbour-sum state (14 VGPRs, +4
+                              VALU ops per word-generation, tb_depth <= 16,
+                              <= 8 with word_planes 4); 3 = as 1 with a
                               step-major schedule (for A/B measurements) */
     uint32_t streams;      /* gol_create, GLOBAL only: split the field into this
                               many row stripes advanced on their own streams of
@@ -87,7 +88,12 @@ typedef struct gol_config {
     uint32_t strip_lanes;  /* lanes per column strip of the stencil kernel: 64, 32
                               or 16 (2 of them halo, 64/L strips per wavefront);
                               0 = auto (narrow strips for short stripes) */
-    uint32_t reserved[1];
+    uint32_t word_planes;  /* cell planes per lane of the stencil kernel: 2 (one
+                              word = 64 columns per lane, every tb_depth) or 4
+                              (two words = 128 columns per lane: half the lane
+                              moves and funnel shifts per cell; tb_depth <= 16);
+                              0 = auto (4 with tb_depth 8 on stripes of 32768+
+                              rows, else 2) */
 } gol_config;
 
 typedef struct gol_engine gol_engine;
@@ -154,8 +160,10 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0,
                     uint32_t* rows_per_wave);
 
 /* Launch plan of a full-depth launch as chosen (strip width in lanes, rows per
- * wavefront); a composite engine reports its first stripe's plan. */
-gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave);
+ * wavefront, planes per lane); a composite engine reports its first stripe's
+ * plan.  Any out pointer may be NULL. */
+gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave,
+                         uint32_t* word_planes);
 
 /* ---- Multi-GPU, one process per GPU (replaces the MPI stripes :70-81 and the
  * halo exchange :104-145 with RCCL send/recv over xGMI) ---- */

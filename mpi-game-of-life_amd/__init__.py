@@ -52,7 +52,7 @@ class Config(ctypes.Structure):
         ("kernel_variant", ctypes.c_uint32),
         ("streams", ctypes.c_uint32),
         ("strip_lanes", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 1),
+        ("word_planes", ctypes.c_uint32),
     ]
 
 
@@ -119,7 +119,7 @@ def lib():
     L.gol_create_group.argtypes = [u64, u64, ctypes.POINTER(Config), i32,
                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp)]
     L.gol_group_step.argtypes = [ctypes.POINTER(vp), i32, u64]
-    L.gol_plan_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    L.gol_plan_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     for name in ["gol_create", "gol_create_rank", "gol_load_ascii", "gol_store_ascii",
                  "gol_load_packed", "gol_store_packed", "gol_init_random", "gol_step",
                  "gol_sync", "gol_digest", "gol_set_timing", "gol_get_timing",
@@ -136,7 +136,8 @@ def _check(st):
 
 
 def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_depth=0,
-                halo_depth=0, rows_per_wave=0, kernel_variant=0, streams=0, strip_lanes=0):
+                halo_depth=0, rows_per_wave=0, kernel_variant=0, streams=0, strip_lanes=0,
+                word_planes=0):
     c = Config()
     lib().gol_config_init(ctypes.byref(c))
     c.birth_mask, c.survive_mask = rule
@@ -149,6 +150,7 @@ def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_
     c.kernel_variant = kernel_variant
     c.streams = streams
     c.strip_lanes = strip_lanes
+    c.word_planes = word_planes
     return c
 
 
@@ -169,11 +171,11 @@ class Engine:
 
     def __init__(self, h, w, rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1,
                  tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None,
-                 kernel_variant=0, streams=0, strip_lanes=0, _handle=None):
+                 kernel_variant=0, streams=0, strip_lanes=0, word_planes=0, _handle=None):
         self.h, self.w = h, w
         self.wq = (w + 63) // 64
         cfg = make_config(rule, device, semantics, ref_ranks, tb_depth, halo_depth,
-                          rows_per_wave, kernel_variant, streams, strip_lanes)
+                          rows_per_wave, kernel_variant, streams, strip_lanes, word_planes)
         handle = ctypes.c_void_p()
         if _handle is not None:
             handle = _handle
@@ -192,9 +194,10 @@ class Engine:
                               ctypes.byref(rpw)))
         self.row0, self.rows, self.tb_depth, self.halo_depth = r0.value, rows.value, k.value, hx.value
         self.rows_per_wave = rpw.value
-        sl, rp = ctypes.c_uint32(), ctypes.c_uint32()
-        _check(lib().gol_plan_info(self._h, ctypes.byref(sl), ctypes.byref(rp)))
+        sl, rp, wp = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().gol_plan_info(self._h, ctypes.byref(sl), ctypes.byref(rp), ctypes.byref(wp)))
         self.strip_lanes = sl.value
+        self.word_planes = wp.value
 
     def close(self):
         if self._h:
@@ -268,10 +271,11 @@ class Group:
     share a GPU."""
 
     def __init__(self, h, w, nranks, devices=None, rule=REF_RULE, tb_depth=0, halo_depth=0,
-                 rows_per_wave=0, kernel_variant=0, strip_lanes=0):
+                 rows_per_wave=0, kernel_variant=0, strip_lanes=0, word_planes=0):
         self.h, self.w, self.n = h, w, nranks
         cfg = make_config(rule, -1 if devices else 0, SEM_GLOBAL, 1, tb_depth, halo_depth,
-                          rows_per_wave, kernel_variant, strip_lanes=strip_lanes)
+                          rows_per_wave, kernel_variant, strip_lanes=strip_lanes,
+                          word_planes=word_planes)
         hs = (ctypes.c_void_p * nranks)()
         devs = (ctypes.c_int * nranks)(*(devices or [0] * nranks))
         _check(lib().gol_create_group(h, w, ctypes.byref(cfg), nranks, devs, hs))

@@ -30,21 +30,52 @@ thread_local std::string g_last_error;
 // profiles/r01/group_bench_*.jsonl)
 constexpr uint64_t kCompositeMinRows = 32768;
 
-// Auto fused depth of the total-sum kernel.  K = 16 (202 VGPRs, 2 waves/SIMD,
-// enough for full VALU issue) for stripes of more than 6144 rows: 124.5 TCUPS at
-// 65536^2 vs 122.4 (K = 8, 4 waves/SIMD) and 106.0 (K = 12), 92 vs 80 / 79 at
-// 8192x65536; K >= 20 drops to 1 wave/SIMD (half issue rate) and loses 30-35%
-// (profiles/r01/sweep_total_sum_depth.jsonl).  Short fields are launch-latency
-// bound and keep K = 8 (4096^2: 11.6 vs 8.7 TCUPS at K = 16).  Rules other than
-// B/S2 and B3/S23 evaluate a 10-term mask sum whose K = 16 state spills: K = 12.
-uint32_t auto_depth(uint64_t rows, const gol_config* cfg)
+// Auto launch layout: fused depth K and planes per lane group (bitlayout.h).
+//  * 2 planes (one word per lane), K = 16 (202 VGPRs, 2 waves/SIMD, enough for
+//    full VALU issue) for stripes of more than 6144 rows: 124.5 TCUPS at 65536^2
+//    vs 122.4 (K = 8, 4 waves/SIMD) and 106.0 (K = 12), 92 vs 80 / 79 at
+//    8192x65536; K >= 20 drops to 1 wave/SIMD (half issue rate) and loses 30-35%
+//    (profiles/r01/sweep_total_sum_depth.jsonl).
+//  * 4 planes (two words per lane: 17% fewer VALU issue slots per cell, but K = 8
+//    to keep 2 waves/SIMD at 236 VGPRs) for stripes of 32768+ rows: +1.3-1.5% at
+//    65536^2 (127.1 vs 125.5 TCUPS with 2 stripe streams, 119.4 vs 117.7 with
+//    one), -3% at 16384 rows and -7% at 8192, where the shorter row blocks of the
+//    wider lanes cost more halo recompute (profiles/r01/sweep_word_planes.jsonl).
+//  * Short fields are launch-latency bound and keep K = 8 with 2 planes (4096^2:
+//    11.0-11.6 TCUPS vs 8.7 at K = 16 and 8.1 with 4 planes).
+//  * Rules other than B/S2 and B3/S23 evaluate a 10-term mask sum whose K = 16
+//    state spills: K = 12.
+// Explicit tb_depth / word_planes / kernel_variant settings are kept; a missing
+// one is filled in to match (4 planes only with depth <= 16).
+struct Layout {
+    uint32_t K;
+    int planes;
+};
+
+Layout auto_layout(uint64_t rows, const gol_config* cfg)
 {
-    if (rows <= 6144) return 8u;
     const bool fixed = (cfg->birth_mask == GOL_REF_BIRTH && cfg->survive_mask == GOL_REF_SURVIVE) ||
                        (cfg->birth_mask == GOL_CONWAY_BIRTH &&
                         cfg->survive_mask == GOL_CONWAY_SURVIVE);
-    if (cfg->kernel_variant == 2) return 12u;  // neighbour-sum state: 14 VGPRs per stage
-    return fixed ? 16u : 12u;
+    const bool deflt_var = cfg->kernel_variant == 0 || cfg->kernel_variant == 1;
+    Layout l;
+    if (cfg->tb_depth) {
+        l.K = cfg->tb_depth;
+    } else if (cfg->word_planes == 4) {
+        l.K = 8;
+    } else if (cfg->word_planes == 0 && fixed && deflt_var && rows >= 32768) {
+        l.K = 8;
+        l.planes = 4;
+        return l;
+    } else if (rows <= 6144) {
+        l.K = 8;
+    } else if (cfg->kernel_variant == 2 || !fixed) {
+        l.K = 12;  // neighbour-sum state (14 VGPRs per stage) / generic rules
+    } else {
+        l.K = 16;
+    }
+    l.planes = cfg->word_planes ? (int)cfg->word_planes : 2;
+    return l;
 }
 
 gol_status fail(gol_status st, const std::string& msg)
@@ -112,6 +143,9 @@ struct gol_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     uint64_t H = 0, W = 0, wq = 0, stride = 0, lastmask = 0;
+    int planes = 2;                      // planes per lane group (bitlayout.h)
+    uint64_t ng = 0;                     // lane groups per row
+    uint64_t lastmask_split[2] = {0, 0};  // stored form of the last group's valid bits
     uint32_t birth = 0, survive = 0;
     gol::RuleKind rule = gol::RULE_REF;
     uint32_t K = 8;
@@ -270,11 +304,11 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
 {
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-    const int occ = std::max(1, gol::life_blocks_per_cu((int)e->K, e->rule, e->var));
+    const int occ = std::max(1, gol::life_blocks_per_cu((int)e->K, e->rule, e->var, e->planes));
     for (const auto& r : raw) {
         gol_engine::Plan p;
         p.segs = r;
-        const RowPlan rp = pick_rows_per_wave(r, e->wq, (int)e->K, occ, 4 * cus,
+        const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, occ, 4 * cus,
                                               (int)e->rows_per_wave, e->lane_shift);
         p.rpw = rp.rpw;
         p.groups = rp.groups;
@@ -321,6 +355,12 @@ gol_status check_cfg(const gol_config* cfg)
     if (cfg->kernel_variant == 2 && cfg->tb_depth > 16)
         return fail(GOL_EINVAL, "kernel_variant 2 (neighbour-sum state) needs tb_depth <= 16");
     if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
+    if (cfg->word_planes != 0 && cfg->word_planes != 2 && cfg->word_planes != 4)
+        return fail(GOL_EINVAL, "word_planes must be 0 (auto), 2 or 4");
+    if (cfg->word_planes == 4 && cfg->tb_depth > 16)
+        return fail(GOL_EINVAL, "word_planes 4 needs tb_depth <= 16");
+    if (cfg->word_planes == 4 && cfg->kernel_variant == 2 && cfg->tb_depth > 8)
+        return fail(GOL_EINVAL, "word_planes 4 with kernel_variant 2 needs tb_depth <= 8");
     return GOL_OK;
 }
 
@@ -340,11 +380,25 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->rule = gol::RULE_CONWAY;
     else
         e->rule = gol::RULE_GENERIC;
-    e->K = cfg->tb_depth ? cfg->tb_depth : auto_depth(e->R, cfg);
+    const Layout lay = auto_layout(e->R, cfg);
+    e->K = lay.K;
     e->rows_per_wave = cfg->rows_per_wave;
     e->lane_shift = cfg->strip_lanes == 64 ? 0 : cfg->strip_lanes == 32 ? 1
                   : cfg->strip_lanes == 16 ? 2 : -1;
     e->var = cfg->kernel_variant == 2 ? 1 : cfg->kernel_variant == 3 ? 2 : 0;
+    e->planes = lay.planes;
+    if (!gol::life_has_kernel((int)e->K, e->var, e->planes))
+        return fail(GOL_EINVAL, "no stencil kernel for this tb_depth / kernel_variant / word_planes");
+    {
+        const uint64_t G = (uint64_t)e->planes / 2;
+        e->ng = (e->wq + G - 1) / G;
+        uint64_t c[2] = {0, 0};
+        for (uint64_t j = 0; j < G; ++j) {
+            const uint64_t idx = (e->ng - 1) * G + j;
+            c[j] = idx + 1 < e->wq ? ~0ull : idx + 1 == e->wq ? e->lastmask : 0ull;
+        }
+        gol_split_group(c, e->lastmask_split, e->planes);
+    }
     e->sem = cfg->semantics;
 
     if (cfg->device >= 0) HIP_TRY(hipSetDevice(cfg->device));
@@ -506,8 +560,9 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     a.strips = p.groups;
     a.lane_shift = p.lane_shift;
     a.stride = (int64_t)e->stride;
-    a.wq = (int64_t)e->wq;
-    a.lastmask = gol_split64(e->lastmask);  // the kernel works on column-split words
+    a.ng = (int64_t)e->ng;
+    a.lastmask[0] = e->lastmask_split[0];  // the kernel works on stored (split) words
+    a.lastmask[1] = e->lastmask_split[1];
     a.rows_per_wave = p.rpw;
     a.total_units = p.total_units;
     a.birth = e->birth;
@@ -520,7 +575,7 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         if (st != GOL_OK) return st;
         HIP_TRY(hipEventRecord(e0, s));
     }
-    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->var, s));
+    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->var, e->planes, s));
     if (timed) {
         HIP_TRY(hipEventRecord(e1, s));
         e->ev_pending.push_back({e0, e1});
@@ -594,7 +649,9 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
         // composite: S same-device stripes with deep halos, advanced together
         gol_config c = *cfg;
         c.streams = 1;
-        if (!c.tb_depth) c.tb_depth = auto_depth(h / S, cfg);
+        const Layout lay = auto_layout(h / S, cfg);
+        c.tb_depth = lay.K;
+        c.word_planes = (uint32_t)lay.planes;
         if (!c.halo_depth) c.halo_depth = 16 * c.tb_depth;
         int dev = cfg->device;
         if (dev < 0) {
@@ -676,7 +733,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     e->nranks = nranks;
     e->row0 = row0;
     e->R = rows;
-    const uint32_t K = cfg->tb_depth ? cfg->tb_depth : auto_depth(rows, cfg);
+    const uint32_t K = auto_layout(rows, cfg).K;
     // rounds of halo_depth generations between exchanges (default 8 launches)
     uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 8 * (uint64_t)K;
     if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
@@ -823,10 +880,10 @@ static uint64_t load_rows_needed(const gol_engine* e)
 
 }  // extern "C"
 
-// Host <-> device transfer of the load/store regions.  `canonical` words use the
+// Host <-> device transfer of the load/store regions.  The caller's words use the
 // public bit order (bit j = column 64q+j) and are converted to/from the
-// engine's column-split words (bitlayout.h); otherwise words are already split.
-static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs, bool canonical)
+// engine's lane groups (bitlayout.h).
+static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs)
 {
     HIP_TRY(hipSetDevice(e->device));
     if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
@@ -843,12 +900,14 @@ static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs, bool
         for (uint64_t i = 0; i < r.rows; ++i) {
             const uint64_t* src = words + (urow + i) * rs;
             uint64_t* dst = tmp.data() + i * e->stride;
-            if (canonical) {
-                for (uint64_t q = 0; q < e->wq; ++q)
-                    dst[q] = gol_split64(q == e->wq - 1 ? (src[q] & e->lastmask) : src[q]);
-            } else {
-                for (uint64_t q = 0; q < e->wq; ++q) dst[q] = src[q];
-                dst[e->wq - 1] &= gol_split64(e->lastmask);
+            const uint64_t G = (uint64_t)e->planes / 2;
+            for (uint64_t gq = 0; gq < e->ng; ++gq) {
+                uint64_t c[2] = {0, 0};
+                for (uint64_t j = 0; j < G; ++j) {
+                    const uint64_t q = gq * G + j;
+                    if (q < e->wq) c[j] = q == e->wq - 1 ? (src[q] & e->lastmask) : src[q];
+                }
+                gol_split_group(c, dst + gq * G, e->planes);
             }
         }
         HIP_TRY(hipMemcpyAsync(e->buf[e->cur] + r.buf_row * e->stride, tmp.data(),
@@ -858,7 +917,7 @@ static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs, bool
     return GOL_OK;
 }
 
-static gol_status download(gol_engine* e, uint64_t* words, uint64_t rs, bool canonical)
+static gol_status download(gol_engine* e, uint64_t* words, uint64_t rs)
 {
     HIP_TRY(hipSetDevice(e->device));
     std::vector<uint64_t> tmp;
@@ -871,7 +930,13 @@ static gol_status download(gol_engine* e, uint64_t* words, uint64_t rs, bool can
         for (uint64_t i = 0; i < r.rows; ++i) {
             uint64_t* dst = words + (urow + i) * rs;
             const uint64_t* src = tmp.data() + i * e->stride;
-            for (uint64_t q = 0; q < e->wq; ++q) dst[q] = canonical ? gol_join64(src[q]) : src[q];
+            const uint64_t G = (uint64_t)e->planes / 2;
+            for (uint64_t gq = 0; gq < e->ng; ++gq) {
+                uint64_t c[2];
+                gol_join_group(src + gq * G, c, e->planes);
+                for (uint64_t j = 0; j < G; ++j)
+                    if (gq * G + j < e->wq) dst[gq * G + j] = c[j];
+            }
         }
     }
     return GOL_OK;
@@ -898,7 +963,7 @@ gol_status gol_load_packed(gol_engine* e, const uint64_t* words, uint64_t rs)
         return GOL_OK;
     }
     if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
-    return upload(e, words, rs, true);
+    return upload(e, words, rs);
 }
 
 gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
@@ -936,9 +1001,9 @@ gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
     for (const auto& r : e->load_regions) {
         const uint64_t urow = e->nranks > 1 ? 0 : r.user_row;
         HIP_TRY(gol::launch_ascii_pack(bytes.p + urow * (e->W + 1), (int64_t)r.rows,
-                                       (int64_t)e->W, (int64_t)e->wq,
+                                       (int64_t)e->W, (int64_t)e->ng,
                                        e->buf[e->cur] + r.buf_row * e->stride,
-                                       (int64_t)e->stride, e->d_flag, e->stream));
+                                       (int64_t)e->stride, e->d_flag, e->planes, e->stream));
     }
     int bad = 0;
     HIP_TRY(hipMemcpyAsync(&bad, e->d_flag, sizeof(int), hipMemcpyDeviceToHost, e->stream));
@@ -960,7 +1025,7 @@ gol_status gol_store_packed(gol_engine* e, uint64_t* words, uint64_t rs)
         return GOL_OK;
     }
     if (rs < e->wq) return fail(GOL_EINVAL, "row stride smaller than ceil(w/64)");
-    return download(e, words, rs, true);
+    return download(e, words, rs);
 }
 
 gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
@@ -989,7 +1054,8 @@ gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
         const uint64_t urow = e->nranks > 1 ? 0 : r.user_row;
         HIP_TRY(gol::launch_ascii_unpack(e->buf[e->cur] + r.buf_row * e->stride,
                                          (int64_t)e->stride, (int64_t)r.rows, (int64_t)e->W,
-                                         (int64_t)e->wq, bytes.p + urow * (e->W + 1), e->stream));
+                                         (int64_t)e->ng, bytes.p + urow * (e->W + 1), e->planes,
+                                         e->stream));
     }
     HIP_TRY(hipMemcpyAsync(buf, bytes.p, len, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1016,7 +1082,7 @@ gol_status gol_init_random(gol_engine* e, uint64_t seed)
     for (const auto& r : e->load_regions)
         HIP_TRY(gol::launch_init_random(e->buf[e->cur], (int64_t)e->stride, (int64_t)e->wq,
                                         e->lastmask, (int64_t)r.buf_row, (int64_t)r.glob_row,
-                                        (int64_t)r.rows, seed, e->stream));
+                                        (int64_t)r.rows, seed, e->planes, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     return GOL_OK;
 }
@@ -1281,8 +1347,8 @@ gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
     HIP_TRY(hipMemsetAsync(e->d_acc, 0, 2 * sizeof(unsigned long long), e->stream));
     for (const auto& r : e->user_regions)
         HIP_TRY(gol::launch_digest(e->buf[e->cur], (int64_t)e->stride, (int64_t)e->wq,
-                                   (int64_t)r.buf_row, (int64_t)r.glob_row, (int64_t)r.rows,
-                                   e->d_acc, e->stream));
+                                   (int64_t)e->ng, (int64_t)r.buf_row, (int64_t)r.glob_row,
+                                   (int64_t)r.rows, e->d_acc, e->planes, e->stream));
     unsigned long long acc[2];
     HIP_TRY(hipMemcpyAsync(acc, e->d_acc, sizeof(acc), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1372,10 +1438,13 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uin
     return GOL_OK;
 }
 
-gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave)
+gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave,
+                         uint32_t* word_planes)
 {
     if (!e) return fail(GOL_EINVAL, "null engine");
-    if (!e->parts.empty()) return gol_plan_info(e->parts[0], strip_lanes, rows_per_wave);
+    if (!e->parts.empty())
+        return gol_plan_info(e->parts[0], strip_lanes, rows_per_wave, word_planes);
+    if (word_planes) *word_planes = (uint32_t)e->planes;
     if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
     // rank engines: plans[Hx-1] is the full-round launch over own rows; else plans[0]
     const auto& p = e->nranks > 1 ? e->plans[e->Hx - 1] : e->plans[0];

@@ -30,12 +30,12 @@ struct SegDesc {
 };
 
 // Strips: a strip is L consecutive lanes (L = 64 >> lane_shift: 64, 32 or 16),
-// each holding one 64-bit word of a row; its first and last lane are the
-// horizontal halo (exact for up to 63 fused generations), so a strip outputs
-// L - 2 words.  A wavefront runs 64 / L strips side by side over the same rows:
+// each holding one lane group of a row (NP 32-bit planes = NP/2 words,
+// bitlayout.h); its first and last lane are the horizontal halo (exact for up to
+// 63 fused generations), so a strip outputs L - 2 groups.  A wavefront runs 64 / L strips side by side over the same rows:
 // narrow strips trade 2 halo lanes per strip for more wavefronts per row block,
 // which lets short stripes use longer row blocks (less vertical halo recompute).
-constexpr int kStripOut = 62;  // output words of a full 64-lane strip
+constexpr int kStripOut = 62;  // output lane groups of a full 64-lane strip
 constexpr int kWavesPerBlock = 4;
 // Zeroed guard rows allocated before/after every state buffer so that the
 // streaming loads (K rows of halo + prefetch distance) never leave the allocation.
@@ -50,8 +50,8 @@ struct StepArgs {
     int32_t strips;       // strip groups per row: ceil(ceil(wq / (L-2)) / (64/L))
     int32_t lane_shift;   // L = 64 >> lane_shift lanes per strip (0, 1 or 2)
     int64_t stride;       // words per buffer row
-    int64_t wq;           // words per field row = ceil(w / 64)
-    uint64_t lastmask;    // valid bits of word wq-1
+    int64_t ng;           // lane groups per field row = ceil(ceil(w / 64) / (NP/2))
+    uint64_t lastmask[2]; // stored-form valid bits of the last group's words
     int64_t rows_per_wave;
     int64_t total_units;  // wavefronts in the launch
     uint32_t birth, survive;
@@ -60,35 +60,38 @@ struct StepArgs {
 // Fused depths with an instantiated kernel, largest first.
 constexpr int kDepthList[] = {32, 24, 20, 16, 12, 8, 7, 6, 4, 2, 1};
 
-// Launch `depth` fused generations (depth in kDepthList).  `var` = kernel variant:
-// 0 total-sum stage state (10 dwords per fused generation), anti-diagonal
-// schedule (default); 1 neighbour-sum state (14 dwords, +4 VALU ops per
-// word-generation; depth <= 16), anti-diagonal; 2 as 0 with the step-major
-// schedule (kept for A/B measurements).
-hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int var, hipStream_t s);
+// Launch `depth` fused generations (depth in kDepthList) on lane groups of
+// `planes` (2 or 4) planes.  `var` = kernel variant: 0 total-sum stage state (5
+// planes per fused generation), anti-diagonal schedule (default); 1
+// neighbour-sum state (7 planes, +4 VALU ops per plane-generation),
+// anti-diagonal; 2 as 0 with the step-major schedule (kept for A/B
+// measurements).  life_has_kernel tells which combinations exist.
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int var, int planes,
+                       hipStream_t s);
+bool life_has_kernel(int depth, int var, int planes);
 
 // Resident 256-thread blocks per CU of the stencil kernel for (depth, rule,
-// variant) -- each block is one wavefront per SIMD (occupancy query).
-int life_blocks_per_cu(int depth, RuleKind rule, int var);
+// variant, planes) -- each block is one wavefront per SIMD (occupancy query).
+int life_blocks_per_cu(int depth, RuleKind rule, int var, int planes);
 
 // Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field
 // rows [glob_row0, glob_row0+nrows).
 hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_t lastmask,
                               int64_t row_base, int64_t glob_row0, int64_t nrows,
-                              uint64_t seed, hipStream_t s);
+                              uint64_t seed, int planes, hipStream_t s);
 
-// ASCII codec: `rows` lines of w cell bytes + '\n' (device memory) <-> column-split
-// words at dst/src with `stride` words per row.  *bad is set if a line does not
-// end in '\n' at byte w.
-hipError_t launch_ascii_pack(const char* src, int64_t rows, int64_t w, int64_t wq, uint64_t* dst,
-                             int64_t stride, int* bad, hipStream_t s);
+// ASCII codec: `rows` lines of w cell bytes + '\n' (device memory) <-> stored
+// lane groups (ng per row) at dst/src with `stride` words per row.  *bad is set
+// if a line does not end in '\n' at byte w.
+hipError_t launch_ascii_pack(const char* src, int64_t rows, int64_t w, int64_t ng, uint64_t* dst,
+                             int64_t stride, int* bad, int planes, hipStream_t s);
 hipError_t launch_ascii_unpack(const uint64_t* src, int64_t stride, int64_t rows, int64_t w,
-                               int64_t wq, char* dst, hipStream_t s);
+                               int64_t ng, char* dst, int planes, hipStream_t s);
 
 // Adds popcount and hash of buffer rows [row_base, row_base+nrows) (field rows
 // glob_row0..) into acc[0], acc[1].
-hipError_t launch_digest(const uint64_t* buf, int64_t stride, int64_t wq, int64_t row_base,
-                         int64_t glob_row0, int64_t nrows, unsigned long long* acc,
-                         hipStream_t s);
+hipError_t launch_digest(const uint64_t* buf, int64_t stride, int64_t wq, int64_t ng,
+                         int64_t row_base, int64_t glob_row0, int64_t nrows,
+                         unsigned long long* acc, int planes, hipStream_t s);
 
 }  // namespace gol

@@ -6,15 +6,17 @@
 // launch (temporal blocking).
 //
 // Kernel shape (one wavefront = one work unit, no LDS, no barriers):
-//   * A wavefront owns a strip of 64 consecutive words of a row (lane l holds
-//     word strip*62 - 1 + l); lanes 0 and 63 are the horizontal halo, so each
-//     strip outputs 62 words.  Words are column-split (bitlayout.h: even columns
-//     in the low dword, odd in the high), so two of the four horizontal
-//     neighbour planes are free; the other two are one v_alignbit each, with the
-//     carry bit from the adjacent lane by a DPP wave shift (wave_shr:1 /
-//     wave_shl:1).  After g fused generations the contamination from the unknown
-//     words beyond the halo lanes has moved g bits into lanes 0/63, so K <= 63
-//     keeps lanes 1..62 exact.
+//   * A wavefront owns a strip of 64 consecutive lane groups of a row (lane l
+//     holds group strip*62 - 1 + l); lanes 0 and 63 are the horizontal halo, so
+//     each strip outputs 62 groups.  A lane group is NP = 2 or 4 planes of 32
+//     cells (bitlayout.h: column NP*j + k of the group at bit j of plane k), so
+//     the horizontal neighbours of every plane but the first and last are other
+//     planes at the same bit; those two take one v_alignbit each, with the carry
+//     bit from the adjacent lane by a DPP wave shift (wave_shr:1 / wave_shl:1).
+//     NP = 4 (two words per lane) pays that once per 128 columns.  After g fused
+//     generations the contamination from the unknown groups beyond the halo
+//     lanes has moved g columns into lanes 0/63, so K <= 63 keeps lanes 1..62
+//     exact.
 //   * The wavefront streams down `rows_per_wave` output rows of its strip, K rows
 //     of vertical halo on each side.  Generation g (1..K) is a pipeline stage that
 //     keeps a 3-row window in registers: for each incoming row it forms the
@@ -38,23 +40,10 @@
 #ifndef GOL_WARM_ROLLED
 #define GOL_WARM_ROLLED 0
 #endif
-#ifndef GOL_HORIZ_BPERM
-#define GOL_HORIZ_BPERM 0
-#endif
-#ifndef GOL_HORIZ_ADDC
-#define GOL_HORIZ_ADDC 0
-#endif
-#ifndef GOL_HORIZ_OR_DPP
-#define GOL_HORIZ_OR_DPP 0
-#endif
 
 namespace gol {
 
 namespace {
-
-struct u2 {
-    uint32_t lo, hi;
-};
 
 __device__ __forceinline__ uint32_t lane_from_left(uint32_t v)
 {
@@ -67,15 +56,38 @@ __device__ __forceinline__ uint32_t lane_from_right(uint32_t v)
     return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xf, 0xf, true);
 }
 
-// Per-generation pipeline stage state (all bit-sliced, two 32-bit halves):
-//   H3 of row r-2 (sum, carry), H3 of row r-1, H2 of row r-1, cells of row r-1,
-// where r is the incoming row.
-struct Stage {
-    u2 ps, pc;
-    u2 cs, cc;
-    u2 hs, hc;
-    u2 al;
+// The NP 32-bit cell planes of one lane group (bitlayout.h): NP/2 words, 32*NP
+// columns; plane k bit j = column NP*j + k of the group.
+template <int NP>
+struct Pl {
+    uint32_t v[NP];
 };
+
+// The group's words as stored in HBM: one 8- (NP = 2) or 16-byte (NP = 4) access.
+template <int NP>
+struct alignas(4 * NP) Grp {
+    uint64_t w[NP / 2];
+};
+
+template <int NP>
+__device__ __forceinline__ Pl<NP> planes_of(const Grp<NP>& g)
+{
+    Pl<NP> p;
+#pragma unroll
+    for (int i = 0; i < NP / 2; ++i) {
+        p.v[2 * i] = (uint32_t)g.w[i];
+        p.v[2 * i + 1] = (uint32_t)(g.w[i] >> 32);
+    }
+    return p;
+}
+template <int NP>
+__device__ __forceinline__ Grp<NP> words_of(const Pl<NP>& p)
+{
+    Grp<NP> g;
+#pragma unroll
+    for (int i = 0; i < NP / 2; ++i) g.w[i] = ((uint64_t)p.v[2 * i + 1] << 32) | p.v[2 * i];
+    return g;
+}
 
 // v_bitop3_b32: any 3-input bitwise function in one VALU op.  The immediate is
 // the function's truth table evaluated on S0 = 0xF0, S1 = 0xCC, S2 = 0xAA.
@@ -126,85 +138,64 @@ __device__ __forceinline__ uint32_t rule32(uint32_t as, uint32_t ac, uint32_t bs
     }
 }
 
-// Horizontal neighbour planes of a column-split word x (bitlayout.h): lo = even
-// columns, hi = odd columns.  An even column's right neighbour and an odd
-// column's left neighbour are the other half at the same bit; the remaining two
-// planes take one funnel shift each, with the carry bit from the adjacent lane.
-struct Horiz {
-    uint32_t Le, Ro;  // left of the even columns, right of the odd columns
+// Horizontal neighbours of a lane group x (bitlayout.h).  Plane k's left
+// neighbours are plane k-1 and its right neighbours plane k+1, at the same bit,
+// except at the two ends: plane 0's left neighbours are plane NP-1 shifted up one
+// bit (its bit 0 from the last plane of the group to the left, in lane l-1), and
+// plane NP-1's right neighbours are plane 0 shifted down one bit (bit 31 from
+// lane l+1).  One DPP wave shift and one v_alignbit each, per group.
+struct Ends {
+    uint32_t l0, rn;
 };
-__device__ __forceinline__ Horiz horiz(u2 x)
+template <int NP>
+__device__ __forceinline__ Ends ends(const Pl<NP>& x)
 {
-#if GOL_HORIZ_BPERM
-    // neighbour lanes through the LDS crossbar (ds_bpermute) instead of DPP moves,
-    // which issue on the VALU at half rate; byte address of lane l-1 / l+1
-    const int lane4 = (int)__lane_id() * 4;
-    const uint32_t hp = (uint32_t)__builtin_amdgcn_ds_bpermute(lane4 - 4, (int)x.hi);
-#if GOL_HORIZ_BPERM == 2  // one direction each way: LDS crossbar and DPP
-    const uint32_t ln = lane_from_right(x.lo);
-#else
-    const uint32_t ln = (uint32_t)__builtin_amdgcn_ds_bpermute(lane4 + 4, (int)x.lo);
-#endif
-    Horiz h;
-    h.Le = __builtin_amdgcn_alignbit(x.hi, hp, 31);
-    h.Ro = __builtin_amdgcn_alignbit(ln, x.lo, 1);
-    return h;
-#elif GOL_HORIZ_ADDC
-    // left shift with the carry from lane l-1 as an add-with-carry: the carries of
-    // all lanes are one wave mask (v_cmp), moved up one lane on the scalar unit
-    const uint64_t m = __builtin_amdgcn_ballot_w64((int32_t)x.hi < 0) << 1;
-    uint32_t le;
-    uint64_t co;
-    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(le), "=s"(co) : "v"(x.hi), "s"(m));
-    const uint32_t ln = lane_from_right(x.lo);
-    Horiz h;
-    h.Le = le;
-    h.Ro = __builtin_amdgcn_alignbit(ln, x.lo, 1);
-    return h;
-#elif GOL_HORIZ_OR_DPP
-    // the carry bit is shifted into place in the neighbour lane and merged by a
-    // v_or_b32 whose src0 reads it through DPP (the mov folds into the or)
-    // (the shifts are opaque asm so the compiler cannot commute them with the lane
-    // move and form a half-rate v_lshl_or_b32 instead)
-    uint32_t th, tl, sh, sl;
-    asm("v_lshrrev_b32 %0, 31, %1" : "=v"(th) : "v"(x.hi));
-    asm("v_lshlrev_b32 %0, 31, %1" : "=v"(tl) : "v"(x.lo));
-    asm("v_lshlrev_b32 %0, 1, %1" : "=v"(sh) : "v"(x.hi));
-    asm("v_lshrrev_b32 %0, 1, %1" : "=v"(sl) : "v"(x.lo));
-    Horiz h;
-    h.Le = sh | lane_from_left(th);
-    h.Ro = sl | lane_from_right(tl);
-    return h;
-#else
-    const uint32_t hp = lane_from_left(x.hi);   // odd columns of word q-1 (bit 31: col 64q-1)
-    const uint32_t ln = lane_from_right(x.lo);  // even columns of word q+1 (bit 0: col 64q+64)
-    Horiz h;
-    h.Le = __builtin_amdgcn_alignbit(x.hi, hp, 31);  // (hi << 1) | (hp >> 31)
-    h.Ro = __builtin_amdgcn_alignbit(ln, x.lo, 1);   // (lo >> 1) | (ln << 31)
-    return h;
-#endif
+    const uint32_t hp = lane_from_left(x.v[NP - 1]);  // bit 31: the column left of the group
+    const uint32_t ln = lane_from_right(x.v[0]);      // bit 0: the column right of the group
+    Ends e;
+    e.l0 = __builtin_amdgcn_alignbit(x.v[NP - 1], hp, 31);  // (last << 1) | (hp >> 31)
+    e.rn = __builtin_amdgcn_alignbit(ln, x.v[0], 1);        // (first >> 1) | (ln << 31)
+    return e;
+}
+template <int NP>
+__device__ __forceinline__ uint32_t left_of(const Pl<NP>& x, const Ends& e, int k)
+{
+    return k == 0 ? e.l0 : x.v[k - 1];
+}
+template <int NP>
+__device__ __forceinline__ uint32_t right_of(const Pl<NP>& x, const Ends& e, int k)
+{
+    return k == NP - 1 ? e.rn : x.v[k + 1];
 }
 
+// Per-generation pipeline stage state, neighbour-sum form (kernel variant 1):
+// H3 (3-cell horizontal sum, bit-sliced sum + carry) of rows r-2 and r-1, H2
+// (centre excluded) and the cells of row r-1, where r is the incoming row.
+template <int NP>
+struct Stage {
+    Pl<NP> ps, pc;
+    Pl<NP> cs, cc;
+    Pl<NP> hs, hc;
+    Pl<NP> al;
+};
+
 // One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
-template <int RULE>
-__device__ __forceinline__ u2 stage_step(Stage& st, u2 x, uint32_t birth, uint32_t survive)
+template <int RULE, int NP>
+__device__ __forceinline__ Pl<NP> stage_step(Stage<NP>& st, const Pl<NP>& x, uint32_t birth,
+                                             uint32_t survive)
 {
-    const Horiz hz = horiz(x);
-    // even half: (L, C, R) = (Le, lo, hi); odd half: (lo, hi, Ro)
-    u2 s2, c2, s3, c3;
-    s2.lo = hz.Le ^ x.hi;
-    c2.lo = hz.Le & x.hi;
-    s3.lo = lop3<kXor3>(hz.Le, x.lo, x.hi);
-    c3.lo = lop3<kMaj>(hz.Le, x.lo, x.hi);
-    s2.hi = x.lo ^ hz.Ro;
-    c2.hi = x.lo & hz.Ro;
-    s3.hi = lop3<kXor3>(x.lo, x.hi, hz.Ro);
-    c3.hi = lop3<kMaj>(x.lo, x.hi, hz.Ro);
-    u2 y;
-    y.lo = rule32<RULE>(st.ps.lo, st.pc.lo, st.hs.lo, st.hc.lo, s3.lo, c3.lo, st.al.lo, birth,
-                        survive);
-    y.hi = rule32<RULE>(st.ps.hi, st.pc.hi, st.hs.hi, st.hc.hi, s3.hi, c3.hi, st.al.hi, birth,
-                        survive);
+    const Ends e = ends(x);
+    Pl<NP> s2, c2, s3, c3, y;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const uint32_t L = left_of(x, e, k), R = right_of(x, e, k);
+        s2.v[k] = L ^ R;
+        c2.v[k] = L & R;
+        s3.v[k] = lop3<kXor3>(L, x.v[k], R);
+        c3.v[k] = lop3<kMaj>(L, x.v[k], R);
+        y.v[k] = rule32<RULE>(st.ps.v[k], st.pc.v[k], st.hs.v[k], st.hc.v[k], s3.v[k], c3.v[k],
+                              st.al.v[k], birth, survive);
+    }
     st.ps = st.cs;
     st.pc = st.cc;
     st.cs = s3;
@@ -215,18 +206,19 @@ __device__ __forceinline__ u2 stage_step(Stage& st, u2 x, uint32_t birth, uint32
     return y;
 }
 
-// Total-sum stage state (10 dwords): H3 of rows r-2 and r-1 and the cells of row
-// r-1.  The emitted cell sees T = H3(r-2) + H3(r-1) + H3(r), the 9-cell sum
-// including itself, so no centre-excluded H2 is formed: 4 VALU ops per word and
-// 4 VGPRs per stage fewer than Stage.  For an alive cell T = n + 1, for a dead
-// one T = n (generic masks: survive bit T-1 / birth bit T); the two fixed rules
-// read it off directly:
+// Total-sum stage state (5 planes per fused generation): H3 of rows r-2 and r-1
+// and the cells of row r-1.  The emitted cell sees T = H3(r-2) + H3(r-1) + H3(r),
+// the 9-cell sum including itself, so no centre-excluded H2 is formed: 4 VALU
+// ops and 2 planes per stage fewer than Stage.  For an alive cell T = n + 1, for
+// a dead one T = n (generic masks: survive bit T-1 / birth bit T); the two fixed
+// rules read it off directly:
 //   REF (B/S2):      next = alive && T == 3
 //   CONWAY (B3/S23): next = T == 3 || (alive && T == 4)
+template <int NP>
 struct StageT {
-    u2 ps, pc;
-    u2 cs, cc;
-    u2 al;
+    Pl<NP> ps, pc;
+    Pl<NP> cs, cc;
+    Pl<NP> al;
 };
 constexpr uint32_t kAnd3 = 0x80;     // a & b & c
 constexpr uint32_t kFour = 0x42;     // ~(a ^ b) & (a ^ c)
@@ -251,7 +243,7 @@ __device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint3
         return lop3<kAnd3>(alive, s0, three);
     } else if constexpr (RULE == RULE_CONWAY) {
         // T == 4  <=>  !s0 && (p + k0 == 2 && !mj  ||  p + k0 == 0 && mj); all
-        // three steps are v_bitop3 (8-byte encodings, see loop_pad.h)
+        // three steps are v_bitop3 (8-byte encodings, see loop_place.h)
         const uint32_t four = lop3<kFour>(p, k0, mj);
         const uint32_t stay = lop3<kAndNot>(alive, four, s0);  // alive & four & !s0
         return lop3<kOrAnd2>(s0, three, stay);                 // (s0 & three) | stay
@@ -275,20 +267,20 @@ __device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint3
     }
 }
 
-template <int RULE>
-__device__ __forceinline__ u2 stage_step(StageT& st, u2 x, uint32_t birth, uint32_t survive)
+template <int RULE, int NP>
+__device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, uint32_t birth,
+                                             uint32_t survive)
 {
-    const Horiz hz = horiz(x);
-    u2 s3, c3;
-    s3.lo = lop3<kXor3>(hz.Le, x.lo, x.hi);
-    c3.lo = lop3<kMaj>(hz.Le, x.lo, x.hi);
-    s3.hi = lop3<kXor3>(x.lo, x.hi, hz.Ro);
-    c3.hi = lop3<kMaj>(x.lo, x.hi, hz.Ro);
-    u2 y;
-    y.lo = rule32_total<RULE>(st.ps.lo, st.pc.lo, st.cs.lo, st.cc.lo, s3.lo, c3.lo, st.al.lo,
-                                  birth, survive);
-    y.hi = rule32_total<RULE>(st.ps.hi, st.pc.hi, st.cs.hi, st.cc.hi, s3.hi, c3.hi, st.al.hi,
-                                  birth, survive);
+    const Ends e = ends(x);
+    Pl<NP> s3, c3, y;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const uint32_t L = left_of(x, e, k), R = right_of(x, e, k);
+        s3.v[k] = lop3<kXor3>(L, x.v[k], R);
+        c3.v[k] = lop3<kMaj>(L, x.v[k], R);
+        y.v[k] = rule32_total<RULE>(st.ps.v[k], st.pc.v[k], st.cs.v[k], st.cc.v[k], s3.v[k],
+                                    c3.v[k], st.al.v[k], birth, survive);
+    }
     st.ps = st.cs;
     st.pc = st.cc;
     st.cs = s3;
@@ -299,19 +291,44 @@ __device__ __forceinline__ u2 stage_step(StageT& st, u2 x, uint32_t birth, uint3
 
 // VAR: 0 = total-sum state, anti-diagonal schedule; 1 = neighbour-sum state,
 // anti-diagonal; 2 = as 0 with the plain step-major schedule.
-template <int RULE, int VAR>
+template <int VAR, int NP>
 struct StageOf {
-    using type = typename std::conditional<VAR != 1, StageT, Stage>::type;
+    using type = typename std::conditional<VAR != 1, StageT<NP>, Stage<NP>>::type;
 };
 
 constexpr int kPrefetch = 4;
 
+// Code placement directive of a steady-state block (see the kernel): every
+// plane of the block's inputs passes through it.
+#define GOL_PL2(p) "+v"(x[p].v[0]), "+v"(x[p].v[1])
+#define GOL_PL4(p) "+v"(x[p].v[0]), "+v"(x[p].v[1]), "+v"(x[p].v[2]), "+v"(x[p].v[3])
+template <bool PAD, int NP>
+__device__ __forceinline__ void place_block(Pl<NP> (&x)[kPrefetch])
+{
+    static_assert(kPrefetch == 4, "placement asm names 4 inputs");
+    if constexpr (NP == 2) {
+        if constexpr (PAD)
+            asm volatile(".p2align 3\n\ts_nop 0" : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3)
+                         : : "memory");
+        else
+            asm volatile(".p2align 3" : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3) : : "memory");
+    } else {
+        if constexpr (PAD)
+            asm volatile(".p2align 3\n\ts_nop 0" : GOL_PL4(0), GOL_PL4(1), GOL_PL4(2), GOL_PL4(3)
+                         : : "memory");
+        else
+            asm volatile(".p2align 3" : GOL_PL4(0), GOL_PL4(1), GOL_PL4(2), GOL_PL4(3) : : "memory");
+    }
+}
+#undef GOL_PL2
+#undef GOL_PL4
 
-template <int K, int RULE, int VAR>
+template <int K, int RULE, int VAR, int NP>
 __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 {
     constexpr bool kDiagonal = VAR != 2;
     constexpr bool kBirths = RULE != RULE_REF;
+    constexpr int G = NP / 2;  // words per lane group
     const int lane = threadIdx.x & 63;
     const int64_t unit =
         (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -335,10 +352,14 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     const int lin = lane & (L - 1);
     const int strip = (int)(u % a.strips) * (1 << lshift) + sub;
 
+    // lane group of this lane; its column mask (columns >= w are dead)
     const int64_t q = (int64_t)strip * (L - 2) - 1 + lin;
-    const bool qin = (q >= 0) && (q < a.wq);
-    const uint64_t cm = qin ? ((q == a.wq - 1) ? a.lastmask : ~0ull) : 0ull;
-    const uint32_t cmlo = (uint32_t)cm, cmhi = (uint32_t)(cm >> 32);
+    const bool qin = (q >= 0) && (q < a.ng);
+    Pl<NP> cm;
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+        cm.v[k] = qin ? ((q == a.ng - 1) ? (uint32_t)(a.lastmask[k / 2] >> (32 * (k & 1))) : ~0u)
+                      : 0u;
     const int64_t qc = qin ? q : 0;
 
     const int64_t rb = sg.out_lo + blk * a.rows_per_wave;
@@ -346,46 +367,47 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     const int64_t T = (re - rb) + 2 * K;  // input rows streamed
     const int64_t row_first = rb - K;     // local row of step 0
 
-    const uint64_t* inp = a.in + (sg.base_row + row_first) * a.stride + qc;
-    uint64_t* outp = a.out + (sg.base_row + rb) * a.stride + qc;
+    const uint64_t* inp = a.in + (sg.base_row + row_first) * a.stride + qc * G;
+    uint64_t* outp = a.out + (sg.base_row + rb) * a.stride + qc * G;
     const bool st_lane = qin && lin >= 1 && lin <= L - 2;
 
     // field-row validity of local row i (dead border) and buffer-row validity
     const int64_t lo_ok = max((int64_t)0, -sg.glob0);             // first local row in field
     const int64_t hi_ok = min(sg.in_rows, sg.field_h - sg.glob0);  // one past last
 
-    typename StageOf<RULE, VAR>::type st[K];
+    typename StageOf<VAR, NP>::type st[K];
 #pragma unroll
     for (int g = 0; g < K; ++g) st[g] = {};
 
-    uint64_t ring[kPrefetch];
+    Grp<NP> ring[kPrefetch];
 #pragma unroll
-    for (int p = 0; p < kPrefetch; ++p) ring[p] = inp[(int64_t)p * a.stride];
+    for (int p = 0; p < kPrefetch; ++p)
+        ring[p] = *reinterpret_cast<const Grp<NP>*>(inp + (int64_t)p * a.stride);
     const uint64_t* pf = inp + (int64_t)kPrefetch * a.stride;
 
     // input row of step t: dead outside the field / buffer, columns >= w masked
-    auto ingest = [&](int64_t t, uint64_t xv) -> u2 {
+    auto ingest = [&](int64_t t, const Grp<NP>& xv) -> Pl<NP> {
         const int64_t i = row_first + t;
         const bool ok = (i >= lo_ok) && (i < hi_ok);
-        u2 x;
-        x.lo = ok ? ((uint32_t)xv & cmlo) : 0u;
-        x.hi = ok ? ((uint32_t)(xv >> 32) & cmhi) : 0u;
+        Pl<NP> x = planes_of(xv);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) x.v[k] = ok ? (x.v[k] & cm.v[k]) : 0u;
         return x;
     };
     // stage g (generation g+1) at step t: emits local row row_first + t - (g+1)
-    auto stage = [&](int g, int64_t t, u2 x) -> u2 {
+    auto stage = [&](int g, int64_t t, Pl<NP> x) -> Pl<NP> {
         x = stage_step<RULE>(st[g], x, a.birth, a.survive);
         if constexpr (kBirths) {
             const int64_t r = sg.glob0 + row_first + t - (g + 1);  // field row
             const bool rok = (r >= 0) && (r < sg.field_h);
-            x.lo = rok ? (x.lo & cmlo) : 0u;
-            x.hi = rok ? (x.hi & cmhi) : 0u;
+#pragma unroll
+            for (int k = 0; k < NP; ++k) x.v[k] = rok ? (x.v[k] & cm.v[k]) : 0u;
         }
         return x;
     };
-    auto store = [&](int64_t t, u2 x) {
+    auto store = [&](int64_t t, const Pl<NP>& x) {
         if (t >= 2 * K && t < T && st_lane)
-            outp[(t - 2 * K) * a.stride] = ((uint64_t)x.hi << 32) | x.lo;
+            *reinterpret_cast<Grp<NP>*>(outp + (t - 2 * K) * a.stride) = words_of(x);
     };
 
     // One block of kPrefetch steps.  GUARD (warm-up blocks): stage g first emits a
@@ -395,11 +417,11 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     // scalar branch per stage-step).
     auto block = [&](int64_t t0, auto guard) {
         constexpr bool kGuard = decltype(guard)::value;
-        u2 x[kPrefetch];
+        Pl<NP> x[kPrefetch];
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
             x[p] = ingest(t0 + p, ring[p]);
-            ring[p] = *pf;
+            ring[p] = *reinterpret_cast<const Grp<NP>*>(pf);
             pf += a.stride;
         }
         // Code placement (steady-state blocks).  gfx950 issues this kernel's
@@ -410,27 +432,14 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         // registers, 89.6 vs 79.9 TCUPS, profiles/r01/loop_alignment_ab.jsonl).
         // The scheduling barriers keep the 4-byte encodings (loads, ingest masks,
         // SALU, stores) out of the compute, so one alignment directive places
-        // all of it.
+        // all of it: the block's inputs pass through the directive, so the
+        // compute that depends on them cannot be scheduled above it; "memory"
+        // keeps the loads above and the stores below.  The compiler may add a
+        // hazard s_nop after it, so the 4-byte pad that gives the wanted parity
+        // is per kernel: loop_place.h, generated by tools/loop_align.py.
         if constexpr (!kGuard) {
-            // the block's inputs pass through the directive, so the compute that
-            // depends on them cannot be scheduled above it; "memory" keeps the
-            // loads above and the stores below.  The compiler may add a hazard
-            // s_nop after it, so the 4-byte pad that gives the wanted parity is
-            // per kernel: loop_place.h, generated by tools/loop_align.py.
-            static_assert(kPrefetch == 4, "placement asm names 4 inputs");
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (life_loop_pad(K, RULE, VAR))
-                asm volatile(".p2align 3\n\ts_nop 0"
-                             : "+v"(x[0].lo), "+v"(x[0].hi), "+v"(x[1].lo), "+v"(x[1].hi),
-                               "+v"(x[2].lo), "+v"(x[2].hi), "+v"(x[3].lo), "+v"(x[3].hi)
-                             :
-                             : "memory");
-            else
-                asm volatile(".p2align 3"
-                             : "+v"(x[0].lo), "+v"(x[0].hi), "+v"(x[1].lo), "+v"(x[1].hi),
-                               "+v"(x[2].lo), "+v"(x[2].hi), "+v"(x[3].lo), "+v"(x[3].hi)
-                             :
-                             : "memory");
+            place_block<life_loop_pad(K, RULE, VAR, NP) != 0>(x);
             __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (kDiagonal) {
@@ -472,64 +481,89 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     for (int64_t t0 = kWarm; t0 < T; t0 += kPrefetch) block(t0, std::false_type{});
 }
 
-template <int K, int VAR>
-hipError_t launch_depth(const StepArgs& a, RuleKind rule, hipStream_t s)
+// Instantiated stencil kernels: 2 planes per lane group at every depth (the
+// neighbour-sum state up to 16); 4 planes up to depth 16 (neighbour-sum up to 8),
+// where 5 planes x 4 x K state words still fit the register file.
+constexpr bool has_kernel(int K, int VAR, int NP)
 {
-    const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
-    const dim3 block(64 * kWavesPerBlock);
-    switch (rule) {
-    case RULE_REF:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, VAR>), grid, block, 0, s, a);
-        break;
-    case RULE_CONWAY:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, VAR>), grid, block, 0, s, a);
-        break;
-    default:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, VAR>), grid, block, 0, s, a);
-        break;
-    }
-    return hipGetLastError();
+    return NP == 2 ? (VAR != 1 || K <= 16) : (K <= 16 && (VAR != 1 || K <= 8));
 }
 
-template <int K>
+template <int K, int VAR, int NP>
+hipError_t launch_depth(const StepArgs& a, RuleKind rule, hipStream_t s)
+{
+    if constexpr (!has_kernel(K, VAR, NP)) {
+        return hipErrorInvalidValue;
+    } else {
+        const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
+        const dim3 block(64 * kWavesPerBlock);
+        switch (rule) {
+        case RULE_REF:
+            hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, VAR, NP>), grid, block, 0, s, a);
+            break;
+        case RULE_CONWAY:
+            hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, VAR, NP>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, VAR, NP>), grid, block, 0, s, a);
+            break;
+        }
+        return hipGetLastError();
+    }
+}
+
+template <int K, int NP>
 hipError_t launch_variant(const StepArgs& a, RuleKind rule, int var, hipStream_t s)
 {
     switch (var) {
-    case 1:  // the neighbour-sum state exists up to depth 16 (14 VGPRs per stage)
-        if constexpr (K <= 16) return launch_depth<K, 1>(a, rule, s);
-        return hipErrorInvalidValue;
-    case 2: return launch_depth<K, 2>(a, rule, s);
-    default: return launch_depth<K, 0>(a, rule, s);
+    case 1: return launch_depth<K, 1, NP>(a, rule, s);
+    case 2: return launch_depth<K, 2, NP>(a, rule, s);
+    default: return launch_depth<K, 0, NP>(a, rule, s);
     }
 }
 
-template <int K, int VAR>
+template <int K>
+hipError_t launch_planes(const StepArgs& a, RuleKind rule, int var, int planes, hipStream_t s)
+{
+    return planes == 4 ? launch_variant<K, 4>(a, rule, var, s) : launch_variant<K, 2>(a, rule, var, s);
+}
+
+template <int K, int VAR, int NP>
 int occupancy_of(RuleKind rule)
 {
-    int blocks = 0;
-    hipError_t e = hipErrorInvalidValue;
-    const int threads = 64 * kWavesPerBlock;
-    if (rule == RULE_REF)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_REF, VAR>, threads, 0);
-    else if (rule == RULE_CONWAY)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_CONWAY, VAR>, threads, 0);
-    else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_GENERIC, VAR>, threads, 0);
-    return e == hipSuccess ? blocks : 0;
+    if constexpr (!has_kernel(K, VAR, NP)) {
+        return 0;
+    } else {
+        int blocks = 0;
+        hipError_t e = hipErrorInvalidValue;
+        const int threads = 64 * kWavesPerBlock;
+        if (rule == RULE_REF)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &blocks, life_tb_kernel<K, RULE_REF, VAR, NP>, threads, 0);
+        else if (rule == RULE_CONWAY)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &blocks, life_tb_kernel<K, RULE_CONWAY, VAR, NP>, threads, 0);
+        else
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &blocks, life_tb_kernel<K, RULE_GENERIC, VAR, NP>, threads, 0);
+        return e == hipSuccess ? blocks : 0;
+    }
 }
 
 template <int K>
-int occupancy_variant(RuleKind rule, int var)
+int occupancy_planes(RuleKind rule, int var, int planes)
 {
+    if (planes == 4) {
+        switch (var) {
+        case 1: return occupancy_of<K, 1, 4>(rule);
+        case 2: return occupancy_of<K, 2, 4>(rule);
+        default: return occupancy_of<K, 0, 4>(rule);
+        }
+    }
     switch (var) {
-    case 1:
-        if constexpr (K <= 16) return occupancy_of<K, 1>(rule);
-        return 0;
-    case 2: return occupancy_of<K, 2>(rule);
-    default: return occupancy_of<K, 0>(rule);
+    case 1: return occupancy_of<K, 1, 2>(rule);
+    case 2: return occupancy_of<K, 2, 2>(rule);
+    default: return occupancy_of<K, 0, 2>(rule);
     }
 }
 
@@ -541,38 +575,62 @@ __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t idx)
     return z ^ (z >> 31);
 }
 
+// Memory-bound helpers below work per lane group of NP planes (NP/2 words,
+// bitlayout.h); the canonical word index r*wq + c is what the synthetic field
+// and the digest are defined on (gol.h), so they match the oracle's.
+
+template <int NP>
 __global__ __launch_bounds__(256) void init_random_kernel(uint64_t* buf, int64_t stride,
                                                           int64_t wq, uint64_t lastmask,
                                                           int64_t row_base, int64_t glob_row0,
                                                           int64_t nrows, uint64_t seed)
 {
-    const int64_t total = nrows * stride;
+    constexpr int G = NP / 2;
+    const int64_t gpr = stride / G;  // lane groups per buffer row
+    const int64_t total = nrows * gpr;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = k / stride, q = k - i * stride;
-        uint64_t v = 0;
-        if (q < wq) {
-            v = splitmix64_at(seed, (uint64_t)(glob_row0 + i) * (uint64_t)wq + (uint64_t)q);
-            if (q == wq - 1) v &= lastmask;  // canonical mask
+        const int64_t i = k / gpr, gq = k - i * gpr;
+        uint64_t c[2] = {0, 0}, s[2];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int64_t idx = gq * G + j;
+            if (idx < wq) {
+                c[j] = splitmix64_at(seed, (uint64_t)(glob_row0 + i) * (uint64_t)wq + (uint64_t)idx);
+                if (idx == wq - 1) c[j] &= lastmask;  // canonical mask
+            }
         }
-        buf[(row_base + i) * stride + q] = gol_split64(v);
+        gol_split_group(c, s, NP);
+#pragma unroll
+        for (int j = 0; j < G; ++j) buf[(row_base + i) * stride + gq * G + j] = s[j];
     }
 }
 
+template <int NP>
 __global__ __launch_bounds__(256) void digest_kernel(const uint64_t* buf, int64_t stride,
-                                                     int64_t wq, int64_t row_base,
+                                                     int64_t wq, int64_t ng, int64_t row_base,
                                                      int64_t glob_row0, int64_t nrows,
                                                      unsigned long long* acc)
 {
-    const int64_t total = nrows * wq;
+    constexpr int G = NP / 2;
+    const int64_t total = nrows * ng;
     uint64_t live = 0, hash = 0;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = k / wq, q = k - i * wq;
-        const uint64_t v = gol_join64(buf[(row_base + i) * stride + q]);
-        live += (uint64_t)__popcll(v);
-        const uint64_t idx = (uint64_t)(glob_row0 + i) * (uint64_t)wq + (uint64_t)q;
-        hash += splitmix64_at(v ^ splitmix64_at(0, idx), 0);
+        const int64_t i = k / ng, gq = k - i * ng;
+        uint64_t s[2] = {0, 0}, c[2];
+#pragma unroll
+        for (int j = 0; j < G; ++j) s[j] = buf[(row_base + i) * stride + gq * G + j];
+        gol_join_group(s, c, NP);
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int64_t idx = gq * G + j;
+            if (idx < wq) {
+                live += (uint64_t)__popcll(c[j]);
+                const uint64_t h = (uint64_t)(glob_row0 + i) * (uint64_t)wq + (uint64_t)idx;
+                hash += splitmix64_at(c[j] ^ splitmix64_at(0, h), 0);
+            }
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         live += __shfl_xor(live, off);
@@ -584,143 +642,180 @@ __global__ __launch_bounds__(256) void digest_kernel(const uint64_t* buf, int64_
     }
 }
 
-// ASCII codec (data.txt / output.txt bytes <-> column-split words), the
+// ASCII codec (data.txt / output.txt bytes <-> stored lane groups), the
 // device-side replacement of readGridFromFile's parse (:91-99) and
-// writeDataToFile's serialisation (:157-164).  One wavefront per (row, word):
-// lane j reads the byte of column 64q+j (coalesced), __ballot forms the
-// canonical word, lane 0 stores it split.  Byte w of every row must be '\n'.
+// writeDataToFile's serialisation (:157-164).  One wavefront per (row, lane
+// group): lane j reads the byte of column 64c+j of each of the group's words
+// (coalesced), __ballot forms the canonical words, lane 0 stores the group.
+// Byte w of every row must be '\n'.
+template <int NP>
 __global__ __launch_bounds__(256) void ascii_pack_kernel(const char* src, int64_t rows, int64_t w,
-                                                         int64_t wq, uint64_t* dst,
+                                                         int64_t ng, uint64_t* dst,
                                                          int64_t stride, int* bad)
 {
+    constexpr int G = NP / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t total = rows * wq;
+    const int64_t total = rows * ng;
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t k = wave0; k < total; k += nwaves) {
-        const int64_t r = k / wq, q = k - r * wq;
-        const int64_t c = q * 64 + lane;
+        const int64_t r = k / ng, gq = k - r * ng;
         const char* line = src + r * (w + 1);
-        const bool live = c < w && line[c] == '1';
-        const uint64_t word = __ballot(live);
+        uint64_t c[2] = {0, 0}, s[2];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int64_t col = (gq * G + j) * 64 + lane;
+            c[j] = __ballot(col < w && line[col] == '1');
+        }
         if (lane == 0) {
-            dst[r * stride + q] = gol_split64(word);
-            if (q == wq - 1 && line[w] != '\n') atomicOr(bad, 1);
+            gol_split_group(c, s, NP);
+#pragma unroll
+            for (int j = 0; j < G; ++j) dst[r * stride + gq * G + j] = s[j];
+            if (gq == ng - 1 && line[w] != '\n') atomicOr(bad, 1);
         }
     }
 }
 
+template <int NP>
 __global__ __launch_bounds__(256) void ascii_unpack_kernel(const uint64_t* src, int64_t stride,
-                                                           int64_t rows, int64_t w, int64_t wq,
+                                                           int64_t rows, int64_t w, int64_t ng,
                                                            char* dst)
 {
+    constexpr int G = NP / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t total = rows * wq;
+    const int64_t total = rows * ng;
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t k = wave0; k < total; k += nwaves) {
-        const int64_t r = k / wq, q = k - r * wq;
-        const uint64_t word = gol_join64(src[r * stride + q]);
-        const int64_t c = q * 64 + lane;
+        const int64_t r = k / ng, gq = k - r * ng;
+        uint64_t s[2] = {0, 0}, c[2];
+#pragma unroll
+        for (int j = 0; j < G; ++j) s[j] = src[r * stride + gq * G + j];
+        gol_join_group(s, c, NP);
         char* line = dst + r * (w + 1);
-        if (c < w) line[c] = ((word >> lane) & 1) ? '1' : '0';
-        if (q == wq - 1 && lane == 0) line[w] = '\n';
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int64_t col = (gq * G + j) * 64 + lane;
+            if (col < w) line[col] = ((c[j] >> lane) & 1) ? '1' : '0';
+        }
+        if (gq == ng - 1 && lane == 0) line[w] = '\n';
     }
 }
 
 }  // namespace
 
-hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int compact, hipStream_t s)
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int var, int planes,
+                       hipStream_t s)
 {
     if (a.total_units <= 0) return hipSuccess;
 #ifdef GOL_DEV_ONLY_DEPTH  // dev A/B builds: one depth only (fast compile)
     if (depth != GOL_DEV_ONLY_DEPTH) return hipErrorInvalidValue;
-    return launch_variant<GOL_DEV_ONLY_DEPTH>(a, rule, compact, s);
+    return launch_planes<GOL_DEV_ONLY_DEPTH>(a, rule, var, planes, s);
 #else
     switch (depth) {
-    case 1: return launch_variant<1>(a, rule, compact, s);
-    case 2: return launch_variant<2>(a, rule, compact, s);
-    case 4: return launch_variant<4>(a, rule, compact, s);
-    case 6: return launch_variant<6>(a, rule, compact, s);
-    case 7: return launch_variant<7>(a, rule, compact, s);
-    case 8: return launch_variant<8>(a, rule, compact, s);
-    case 12: return launch_variant<12>(a, rule, compact, s);
-    case 16: return launch_variant<16>(a, rule, compact, s);
-    case 20: return launch_variant<20>(a, rule, compact, s);
-    case 24: return launch_variant<24>(a, rule, compact, s);
-    case 32: return launch_variant<32>(a, rule, compact, s);
+    case 1: return launch_planes<1>(a, rule, var, planes, s);
+    case 2: return launch_planes<2>(a, rule, var, planes, s);
+    case 4: return launch_planes<4>(a, rule, var, planes, s);
+    case 6: return launch_planes<6>(a, rule, var, planes, s);
+    case 7: return launch_planes<7>(a, rule, var, planes, s);
+    case 8: return launch_planes<8>(a, rule, var, planes, s);
+    case 12: return launch_planes<12>(a, rule, var, planes, s);
+    case 16: return launch_planes<16>(a, rule, var, planes, s);
+    case 20: return launch_planes<20>(a, rule, var, planes, s);
+    case 24: return launch_planes<24>(a, rule, var, planes, s);
+    case 32: return launch_planes<32>(a, rule, var, planes, s);
     default: return hipErrorInvalidValue;
     }
 #endif
 }
 
-int life_blocks_per_cu(int depth, RuleKind rule, int compact)
+int life_blocks_per_cu(int depth, RuleKind rule, int var, int planes)
 {
 #ifdef GOL_DEV_ONLY_DEPTH
-    return depth == GOL_DEV_ONLY_DEPTH ? occupancy_variant<GOL_DEV_ONLY_DEPTH>(rule, compact) : 0;
+    return depth == GOL_DEV_ONLY_DEPTH ? occupancy_planes<GOL_DEV_ONLY_DEPTH>(rule, var, planes)
+                                       : 0;
 #else
     switch (depth) {
-    case 1: return occupancy_variant<1>(rule, compact);
-    case 2: return occupancy_variant<2>(rule, compact);
-    case 4: return occupancy_variant<4>(rule, compact);
-    case 6: return occupancy_variant<6>(rule, compact);
-    case 7: return occupancy_variant<7>(rule, compact);
-    case 8: return occupancy_variant<8>(rule, compact);
-    case 12: return occupancy_variant<12>(rule, compact);
-    case 16: return occupancy_variant<16>(rule, compact);
-    case 20: return occupancy_variant<20>(rule, compact);
-    case 24: return occupancy_variant<24>(rule, compact);
-    case 32: return occupancy_variant<32>(rule, compact);
+    case 1: return occupancy_planes<1>(rule, var, planes);
+    case 2: return occupancy_planes<2>(rule, var, planes);
+    case 4: return occupancy_planes<4>(rule, var, planes);
+    case 6: return occupancy_planes<6>(rule, var, planes);
+    case 7: return occupancy_planes<7>(rule, var, planes);
+    case 8: return occupancy_planes<8>(rule, var, planes);
+    case 12: return occupancy_planes<12>(rule, var, planes);
+    case 16: return occupancy_planes<16>(rule, var, planes);
+    case 20: return occupancy_planes<20>(rule, var, planes);
+    case 24: return occupancy_planes<24>(rule, var, planes);
+    case 32: return occupancy_planes<32>(rule, var, planes);
     default: return 0;
     }
 #endif
 }
 
+bool life_has_kernel(int depth, int var, int planes) { return has_kernel(depth, var, planes); }
+
+static dim3 grid_for(int64_t items, int64_t per_block, int64_t cap)
+{
+    int64_t blocks = (items + per_block - 1) / per_block;
+    if (blocks > cap) blocks = cap;
+    return dim3((unsigned)blocks);
+}
+
 hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_t lastmask,
                               int64_t row_base, int64_t glob_row0, int64_t nrows, uint64_t seed,
-                              hipStream_t s)
+                              int planes, hipStream_t s)
 {
     if (nrows <= 0) return hipSuccess;
-    const int64_t total = nrows * stride;
-    int64_t blocks = (total + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(init_random_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, stride,
-                       wq, lastmask, row_base, glob_row0, nrows, seed);
+    const dim3 grid = grid_for(nrows * stride / (planes / 2), 256, 8192);
+    if (planes == 4)
+        hipLaunchKernelGGL(init_random_kernel<4>, grid, dim3(256), 0, s, buf, stride, wq, lastmask,
+                           row_base, glob_row0, nrows, seed);
+    else
+        hipLaunchKernelGGL(init_random_kernel<2>, grid, dim3(256), 0, s, buf, stride, wq, lastmask,
+                           row_base, glob_row0, nrows, seed);
     return hipGetLastError();
 }
 
-hipError_t launch_ascii_pack(const char* src, int64_t rows, int64_t w, int64_t wq, uint64_t* dst,
-                             int64_t stride, int* bad, hipStream_t s)
+hipError_t launch_ascii_pack(const char* src, int64_t rows, int64_t w, int64_t ng, uint64_t* dst,
+                             int64_t stride, int* bad, int planes, hipStream_t s)
 {
     if (rows <= 0) return hipSuccess;
-    int64_t blocks = (rows * wq + 3) / 4;
-    if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(ascii_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, w,
-                       wq, dst, stride, bad);
+    const dim3 grid = grid_for(rows * ng, 4, 16384);
+    if (planes == 4)
+        hipLaunchKernelGGL(ascii_pack_kernel<4>, grid, dim3(256), 0, s, src, rows, w, ng, dst,
+                           stride, bad);
+    else
+        hipLaunchKernelGGL(ascii_pack_kernel<2>, grid, dim3(256), 0, s, src, rows, w, ng, dst,
+                           stride, bad);
     return hipGetLastError();
 }
 
 hipError_t launch_ascii_unpack(const uint64_t* src, int64_t stride, int64_t rows, int64_t w,
-                               int64_t wq, char* dst, hipStream_t s)
+                               int64_t ng, char* dst, int planes, hipStream_t s)
 {
     if (rows <= 0) return hipSuccess;
-    int64_t blocks = (rows * wq + 3) / 4;
-    if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(ascii_unpack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, stride,
-                       rows, w, wq, dst);
+    const dim3 grid = grid_for(rows * ng, 4, 16384);
+    if (planes == 4)
+        hipLaunchKernelGGL(ascii_unpack_kernel<4>, grid, dim3(256), 0, s, src, stride, rows, w, ng,
+                           dst);
+    else
+        hipLaunchKernelGGL(ascii_unpack_kernel<2>, grid, dim3(256), 0, s, src, stride, rows, w, ng,
+                           dst);
     return hipGetLastError();
 }
 
-hipError_t launch_digest(const uint64_t* buf, int64_t stride, int64_t wq, int64_t row_base,
-                         int64_t glob_row0, int64_t nrows, unsigned long long* acc,
-                         hipStream_t s)
+hipError_t launch_digest(const uint64_t* buf, int64_t stride, int64_t wq, int64_t ng,
+                         int64_t row_base, int64_t glob_row0, int64_t nrows,
+                         unsigned long long* acc, int planes, hipStream_t s)
 {
     if (nrows <= 0) return hipSuccess;
-    const int64_t total = nrows * wq;
-    int64_t blocks = (total + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(digest_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, stride, wq,
-                       row_base, glob_row0, nrows, acc);
+    const dim3 grid = grid_for(nrows * ng, 256, 8192);
+    if (planes == 4)
+        hipLaunchKernelGGL(digest_kernel<4>, grid, dim3(256), 0, s, buf, stride, wq, ng, row_base,
+                           glob_row0, nrows, acc);
+    else
+        hipLaunchKernelGGL(digest_kernel<2>, grid, dim3(256), 0, s, buf, stride, wq, ng, row_base,
+                           glob_row0, nrows, acc);
     return hipGetLastError();
 }
 

@@ -22,12 +22,15 @@ def test_group_matches_single_field(pkg, oracle, nranks, rule):
     R = {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}[rule]
     h, w = 203, 4000
     g = oracle.bp_random(h, w, 3 + nranks)
-    for tb, hx, gens, kv, lanes in ((8, 0, 37, 1, 0), (4, 12, 30, 1, 0), (2, 5, 11, 1, 0),
-                                    (1, 3, 7, 1, 0), (16, 16, 33, 1, 0), (8, 0, 37, 2, 0),
-                                    (16, 24, 50, 2, 0), (16, 0, 70, 1, 32), (8, 0, 37, 1, 16)):
+    for tb, hx, gens, kv, lanes, wp in ((8, 0, 37, 1, 0, 0), (4, 12, 30, 1, 0, 0),
+                                        (2, 5, 11, 1, 0, 0), (1, 3, 7, 1, 0, 0),
+                                        (16, 16, 33, 1, 0, 0), (8, 0, 37, 2, 0, 0),
+                                        (16, 24, 50, 2, 0, 0), (16, 0, 70, 1, 32, 0),
+                                        (8, 0, 37, 1, 16, 0), (8, 0, 37, 1, 0, 2),
+                                        (16, 0, 40, 1, 0, 4)):
         ref = oracle.bp_run(g, w, gens, R)
         with pkg.Group(h, w, nranks, rule=R, tb_depth=tb, halo_depth=hx,
-                       kernel_variant=kv, strip_lanes=lanes) as grp:
+                       kernel_variant=kv, strip_lanes=lanes, word_planes=wp) as grp:
             grp.load_packed(g)
             grp.step(gens)
             grp.sync()

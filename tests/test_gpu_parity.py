@@ -20,6 +20,14 @@ H, W = GOLD["h"], GOLD["w"]
 DEPTHS = [1, 2, 4, 6, 7, 8, 12, 16, 20, 24, 32]
 
 
+def has_kernel(depth, variant, planes):
+    """Instantiated stencil kernels (life_kernels.hip has_kernel; `variant` is
+    gol_config.kernel_variant: 2 = neighbour-sum state)."""
+    if planes == 2:
+        return variant != 2 or depth <= 16
+    return depth <= 16 and (variant != 2 or depth <= 8)
+
+
 def mask(ns):
     return sum(1 << n for n in ns)
 
@@ -82,31 +90,38 @@ def test_random_fields_every_depth(pkg, oracle, shape, rule):
     g = oracle.bp_random(h, w, seed)
     for gens in (1, 3, 16, 21, 70):
         want[gens] = oracle.bp_run(g, w, gens, R)
-    for depth, variant in [(d, v) for d in DEPTHS for v in (1, 2, 3) if v != 2 or d <= 16]:
+    for depth, variant, planes in [(d, v, p) for d in DEPTHS for v in (1, 2, 3) for p in (2, 4)
+                                   if has_kernel(d, v, p)]:
         for gens, ref in want.items():
             with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth,
-                            kernel_variant=variant) as e:
+                            kernel_variant=variant, word_planes=planes) as e:
+                assert e.word_planes == planes
                 e.init_random(seed)
                 e.step(gens)
                 got = e.store_packed()
-                assert (got == ref).all(), f"depth {depth} variant {variant} gens {gens}"
+                assert (got == ref).all(), f"depth {depth} variant {variant} planes {planes} gens {gens}"
                 assert e.digest() == oracle.bp_digest(ref, w)
 
 
+@pytest.mark.parametrize("planes", [2, 4])
 @pytest.mark.parametrize("lanes", [64, 32, 16])
 @pytest.mark.parametrize("rule", ["ref", "conway", "daynight"])
-def test_strip_widths(pkg, oracle, lanes, rule):
+def test_strip_widths(pkg, oracle, lanes, rule, planes):
     """Narrow strips (32/16 lanes, 2/4 per wavefront): strip seams inside a
-    wavefront, partial last strip groups, every depth class."""
+    wavefront, partial last strip groups, every depth class, both lane-group
+    layouts (odd word counts leave the last 4-plane group half empty)."""
     R = rules(oracle)[rule]
-    for h, w in [(1, 1), (7, 65), (40, 1921), (33, 1983), (129, 4097), (64, 900)]:
+    for h, w in [(1, 1), (7, 65), (40, 1921), (33, 1983), (129, 4097), (64, 900), (9, 3969)]:
         seed = 7 * h + w
         g = oracle.bp_random(h, w, seed)
         for depth in (1, 4, 16, 32):
+            if not has_kernel(depth, 1, planes):
+                continue
             for gens in (3, 33, 70):
                 ref = oracle.bp_run(g, w, gens, R)
-                with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth, strip_lanes=lanes) as e:
-                    assert e.strip_lanes == lanes
+                with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth, strip_lanes=lanes,
+                                word_planes=planes) as e:
+                    assert e.strip_lanes == lanes and e.word_planes == planes
                     e.init_random(seed)
                     e.step(gens)
                     assert (e.store_packed() == ref).all(), f"{h}x{w} depth {depth} gens {gens}"
@@ -120,11 +135,12 @@ def test_row_blocking(pkg, oracle, rpw, variant):
     g = oracle.bp_random(h, w, 5)
     ref = oracle.bp_run(g, w, 16, oracle.CONWAY)
     for lanes in (64, 32, 16):
-        with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw,
-                        kernel_variant=variant, strip_lanes=lanes) as e:
-            e.init_random(5)
-            e.step(16)
-            assert (e.store_packed() == ref).all(), lanes
+        for planes in (2, 4):
+            with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw,
+                            kernel_variant=variant, strip_lanes=lanes, word_planes=planes) as e:
+                e.init_random(5)
+                e.step(16)
+                assert (e.store_packed() == ref).all(), (lanes, planes)
 
 
 def test_load_packed_roundtrip(pkg, oracle):
@@ -155,6 +171,10 @@ def test_ascii_roundtrip_and_errors(pkg, oracle):
         pkg.Engine(0, 5, device=0)
     with pytest.raises(pkg.GolError):
         pkg.Engine(5, 5, device=0, tb_depth=3)
+    with pytest.raises(pkg.GolError):
+        pkg.Engine(5, 5, device=0, tb_depth=20, word_planes=4)
+    with pytest.raises(pkg.GolError):
+        pkg.Engine(5, 5, device=0, word_planes=3)
 
 
 @pytest.mark.parametrize("P", [2, 3, 5, 8])
@@ -258,14 +278,17 @@ def test_timing_sampled(pkg):
     assert t["cell_gens"] == 1024 * 1024 * 24
 
 
-def test_ascii_codec_large_and_malformed(pkg, oracle):
-    """Device ASCII codec (ballot pack / coalesced unpack) on multi-word rows, and
-    a malformed line deep inside the field."""
-    h, w = 333, 4100
+@pytest.mark.parametrize("w", [4100, 4033])
+def test_ascii_codec_large_and_malformed(pkg, oracle, w):
+    """Device ASCII codec (ballot pack / coalesced unpack) on multi-word rows (odd
+    and even word counts), both lane-group layouts, and a malformed line deep
+    inside the field."""
+    h = 333
     g = oracle.bp_random(h, w, 31)
     data = oracle.bp_unpack(g, w)
-    for streams in (1, 2):
-        with pkg.Engine(h, w, device=0, streams=streams, rule=pkg.CONWAY) as e:
+    for streams, planes in ((1, 2), (2, 2), (1, 4), (2, 4)):
+        with pkg.Engine(h, w, device=0, streams=streams, rule=pkg.CONWAY,
+                        word_planes=planes) as e:
             e.load_ascii(data)
             assert (e.store_packed() == g).all()
             assert e.store_ascii() == data

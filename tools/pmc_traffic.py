@@ -37,6 +37,7 @@ def main():
     p.add_argument("--out", default="profiles/traffic.json")
     p.add_argument("--tag", default="")
     p.add_argument("--streams", type=int, default=2, help="engine stripe streams when profiled")
+    p.add_argument("--word-planes", type=int, default=2)
     a = p.parse_args()
     fetch = per_kernel(os.path.join(a.prof_dir, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"),
                        "FETCH_SIZE")
@@ -57,7 +58,7 @@ def main():
     launches = len(fetch["life_tb_kernel"])
     rec = {
         "size": n, "tb_depth": a.tb_depth, "rows_per_wave": a.rows_per_wave, "n_gpus": 1,
-        "streams": a.streams,
+        "streams": a.streams, "word_planes": a.word_planes,
         "hbm_bytes_per_launch": round(rd + wr),
         "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
         "field_bytes": cells // 8,
@@ -71,8 +72,9 @@ def main():
     if os.path.exists(a.out):
         doc = json.load(open(a.out))
     doc["records"] = [r for r in doc["records"]
-                      if not all(r.get(k) == rec[k] for k in ("size", "tb_depth", "rows_per_wave",
-                                                              "n_gpus", "streams"))]
+                      if not all(r.get(k, 2 if k == "word_planes" else None) == rec[k]
+                                 for k in ("size", "tb_depth", "rows_per_wave", "n_gpus",
+                                           "streams", "word_planes"))]
     doc["records"].append(rec)
     doc["_doc"] = ("HBM bytes per life_tb_kernel launch from rocprofv3 FETCH_SIZE / WRITE_SIZE "
                    "(separate passes), calibrated on digest_kernel / init_random_kernel in the "

@@ -17,15 +17,18 @@ import __graft_entry__ as entry  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--size", type=int, default=65536)
-p.add_argument("--tb-depth", type=int, default=8)
+p.add_argument("--tb-depth", type=int, default=0, help="0 = the engine's auto layout")
+p.add_argument("--word-planes", type=int, default=0)
 p.add_argument("--rows-per-wave", type=int, default=0)
 p.add_argument("--launches", type=int, default=4)
 a = p.parse_args()
 pkg = entry.load_package()
-e = pkg.Engine(a.size, a.size, device=0, tb_depth=a.tb_depth, rows_per_wave=a.rows_per_wave)
+e = pkg.Engine(a.size, a.size, device=0, tb_depth=a.tb_depth, rows_per_wave=a.rows_per_wave,
+               word_planes=a.word_planes)
+print("layout", e.tb_depth, e.word_planes)
 e.init_random(1)
 print("digest", e.digest())
-e.step(a.tb_depth * a.launches)
+e.step(e.tb_depth * a.launches)
 e.sync()
 print("digest", e.digest())
 e.close()

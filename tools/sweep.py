@@ -24,6 +24,7 @@ def main():
     p.add_argument("--rpw", default="0")
     p.add_argument("--variants", default="0")
     p.add_argument("--lanes", default="0", help="strip widths (gol_config.strip_lanes)")
+    p.add_argument("--planes", default="0", help="planes per lane group (gol_config.word_planes)")
     p.add_argument("--streams", type=int, default=0, help="gol_config.streams (0 = auto)")
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--rule", default="ref")
@@ -36,15 +37,16 @@ def main():
     variants = list(itertools.product([int(x) for x in a.depths.split(",")],
                                       [int(x) for x in a.rpw.split(",")],
                                       [int(x) for x in a.variants.split(",")],
-                                      [int(x) for x in a.lanes.split(",")]))
+                                      [int(x) for x in a.lanes.split(",")],
+                                      [int(x) for x in a.planes.split(",")]))
     engines = {}
-    for d, r, kv, sl in variants:
+    for d, r, kv, sl, wp in variants:
         e = pkg.Engine(h, w, rule=rule, device=0, tb_depth=d, rows_per_wave=r,
-                       kernel_variant=kv, streams=a.streams, strip_lanes=sl)
+                       kernel_variant=kv, streams=a.streams, strip_lanes=sl, word_planes=wp)
         e.init_random(1)
-        e.step(d)  # warm
+        e.step(d or 8)  # warm
         e.sync()
-        engines[(d, r, kv, sl)] = e
+        engines[(d, r, kv, sl, wp)] = e
         if len(engines) > 6:  # bound HBM use: 1 GiB per engine at 65536^2
             pass
     res = {v: [] for v in variants}
@@ -64,8 +66,10 @@ def main():
     for v in variants:
         r = sorted(res[v])
         med = r[len(r) // 2]
-        print(json.dumps({"tb_depth": v[0], "rows_per_wave": v[1] or f"auto({engines[v].rows_per_wave})",
+        print(json.dumps({"tb_depth": v[0] or f"auto({engines[v].tb_depth})",
+                          "rows_per_wave": v[1] or f"auto({engines[v].rows_per_wave})",
                           "variant": v[2], "strip_lanes": engines[v].strip_lanes,
+                          "word_planes": engines[v].word_planes,
                           "gcups_wall_median": round(med[0], 1),
                           "gcups_wall_best": round(r[-1][0], 1),
                           "kernel_ms_avg": round(med[1], 4),
