@@ -91,3 +91,46 @@ def test_cli_stripes_intended_semantics(pkg, tmp_path, stripes):
     r = run_cli(pkg, d, "--gpus", "1", "--stripes", str(stripes))
     assert r.returncode == 0, r.stderr
     assert hashlib.sha256((d / "output.txt").read_bytes()).hexdigest() == case["sha256"]
+
+
+# ---- gol-mpi: the multi-process launch shape (mpirun -np P, one rank per GPU) ----
+
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+def mpi_cli(pkg):
+    path = os.path.join(os.path.dirname(pkg.CLI_PATH), "gol-mpi")
+    if not (os.path.exists(path) and os.path.exists(MPIRUN)):
+        pytest.skip("gol-mpi not built (no MPI on this host)")
+    return path
+
+
+def run_mpi(pkg, d, np_, *args):
+    return subprocess.run([MPIRUN, "-np", str(np_), mpi_cli(pkg), "--dir", str(d), *args],
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_mpi_cli_usage_and_bad_config(pkg, tmp_path):
+    """Argument and grid_size_data.txt errors end every rank before any GPU call."""
+    r = run_mpi(pkg, tmp_path, 1, "--help")
+    assert r.returncode == 0 and "gol-mpi" in r.stderr
+    (tmp_path / "grid_size_data.txt").write_text("12 x")
+    assert run_mpi(pkg, tmp_path, 2).returncode != 0
+
+
+@pytest.mark.gpu
+def test_mpi_cli_one_rank_matches_reference(pkg, tmp_path):
+    """mpirun -np 1 gol-mpi: RCCL bootstrap over MPI, rank engine, its rows read and
+    written at their offsets -- the reference's -np 1 output, stale tail kept.
+    (Two ranks need two GPUs: RCCL refuses two ranks on one device.)"""
+    case = [c for c in GOLD["cases"] if c["np"] == 1 and c["gens"] == 100][0]
+    d = setup_dir(tmp_path, 100)
+    (d / "output.txt").write_bytes(b"y" * (1500 * 501 + 5))
+    r = run_mpi(pkg, d, 1)
+    assert r.returncode == 0, r.stderr
+    out = (d / "output.txt").read_bytes()
+    assert hashlib.sha256(out[:1500 * 501]).hexdigest() == case["sha256"]
+    assert out[1500 * 501:] == b"y" * 5
+    lines = r.stdout.splitlines()
+    assert lines[0] == "Process 0 wrote data to the file."
+    assert re.fullmatch(r"Total time = [0-9.e+-]+", lines[1])
