@@ -296,17 +296,43 @@ struct StageOf {
     using type = typename std::conditional<VAR != 1, StageT<NP>, Stage<NP>>::type;
 };
 
-constexpr int kPrefetch = 4;
+// Steps per block (rows prefetched ahead through the register ring): 8 for the
+// 2-plane kernels of depth >= 16, whose 2 waves/SIMD have VGPRs to spare (203 ->
+// 230), 4 elsewhere.  In-process A/B at K = 16, 2 planes: +2.5% at 65536^2
+// (129.0 vs 125.8 TCUPS), +0.3% at 8448 rows (profiles/r01/ab_prefetch_depth.jsonl).
+// GOL_PF_NP2 overrides it for dev A/B builds.
+template <int NP, int K>
+constexpr int kPfOf()
+{
+#ifdef GOL_PF_NP2
+    return NP == 2 ? GOL_PF_NP2 : 4;
+#else
+    return (NP == 2 && K >= 16) ? 8 : 4;
+#endif
+}
+#ifndef GOL_DEV_FLIP_PAD  // dev A/B builds: invert loop_place.h's pads
+#define GOL_DEV_FLIP_PAD 0
+#endif
 
 // Code placement directive of a steady-state block (see the kernel): every
 // plane of the block's inputs passes through it.
 #define GOL_PL2(p) "+v"(x[p].v[0]), "+v"(x[p].v[1])
 #define GOL_PL4(p) "+v"(x[p].v[0]), "+v"(x[p].v[1]), "+v"(x[p].v[2]), "+v"(x[p].v[3])
-template <bool PAD, int NP>
-__device__ __forceinline__ void place_block(Pl<NP> (&x)[kPrefetch])
+template <bool PAD, int NP, int PF>
+__device__ __forceinline__ void place_block(Pl<NP> (&x)[PF])
 {
-    static_assert(kPrefetch == 4, "placement asm names 4 inputs");
-    if constexpr (NP == 2) {
+    static_assert((NP == 2 && (PF == 4 || PF == 8)) || (NP == 4 && PF == 4),
+                  "placement asm names 4 or 8 inputs");
+    if constexpr (NP == 2 && PF == 8) {
+        if constexpr (PAD)
+            asm volatile(".p2align 3\n\ts_nop 0"
+                         : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3), GOL_PL2(4), GOL_PL2(5),
+                           GOL_PL2(6), GOL_PL2(7) : : "memory");
+        else
+            asm volatile(".p2align 3"
+                         : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3), GOL_PL2(4), GOL_PL2(5),
+                           GOL_PL2(6), GOL_PL2(7) : : "memory");
+    } else if constexpr (NP == 2) {
         if constexpr (PAD)
             asm volatile(".p2align 3\n\ts_nop 0" : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3)
                          : : "memory");
@@ -329,6 +355,8 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     constexpr bool kDiagonal = VAR != 2;
     constexpr bool kBirths = RULE != RULE_REF;
     constexpr int G = NP / 2;  // words per lane group
+    constexpr int kPrefetch = kPfOf<NP, K>();
+    static_assert(K + 2 * kPrefetch <= kGuardRows, "streaming loads must stay in the guard rows");
     const int lane = threadIdx.x & 63;
     const int64_t unit =
         (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -439,7 +467,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         // is per kernel: loop_place.h, generated by tools/loop_align.py.
         if constexpr (!kGuard) {
             __builtin_amdgcn_sched_barrier(0);
-            place_block<life_loop_pad(K, RULE, VAR, NP) != 0>(x);
+            place_block<(life_loop_pad(K, RULE, VAR, NP) != 0) != (GOL_DEV_FLIP_PAD != 0), NP, kPrefetch>(x);
             __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (kDiagonal) {
