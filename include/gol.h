@@ -92,9 +92,7 @@ typedef struct gol_config {
                               word = 64 columns per lane, every tb_depth) or 4
                               (two words = 128 columns per lane: half the lane
                               moves and funnel shifts per cell; tb_depth <= 16);
-                              0 = auto (4 with tb_depth 8 on the 32768+-row
-                              stripes of a multi-stream gol_create and on
-                              single-stream stripes of 65536+ rows, else 2) */
+                              0 = auto (= 2; 4 only on request) */
 } gol_config;
 
 typedef struct gol_engine gol_engine;

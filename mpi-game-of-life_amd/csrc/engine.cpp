@@ -37,13 +37,12 @@ constexpr uint64_t kCompositeMinRows = 32768;
 //    8192x65536; K >= 20 drops to 1 wave/SIMD (half issue rate) and loses 30-35%
 //    (profiles/r01/sweep_total_sum_depth.jsonl).
 //  * 4 planes (two words per lane: 17% fewer VALU issue slots per cell, but K = 8
-//    to keep 2 waves/SIMD at 236 VGPRs) for the 32768+-row parts of a composite
-//    (2 stripes sharing the GPU) and single-stream stripes of 65536+ rows: +1.3-3%
-//    at 65536^2 (126.8 vs 125.6 TCUPS with 2 stripe streams, 119.4 vs 117.7 with
-//    one), but -6.5% on a lone 33024-row stripe (a 2-GPU rank: 110.1 vs 117.8), -3%
-//    at 16384 rows and -7% at 8192, where the shorter row blocks of the wider lanes
-//    cost more halo recompute (profiles/r01/sweep_word_planes.jsonl,
-//    ab_word_planes_r01.jsonl).
+//    to keep 2 waves/SIMD at 236 VGPRs) only when asked for (word_planes = 4).
+//    Once the 2-plane K = 16 kernel got its 8-step prefetch ring it wins
+//    everywhere: 129.1 vs 123.7 TCUPS at 65536^2 (composite, in-process A/B,
+//    profiles/r01/ab_default_layout_pf8.jsonl), and it was already ahead on lone
+//    stripes of 33024 rows or fewer (profiles/r01/ab_word_planes_r01.jsonl,
+//    sweep_word_planes.jsonl).
 //  * Short fields are launch-latency bound and keep K = 8 with 2 planes (4096^2:
 //    11.0-11.6 TCUPS vs 8.7 at K = 16 and 8.1 with 4 planes).
 //  * Rules other than B/S2 and B3/S23 evaluate a 10-term mask sum whose K = 16
@@ -55,7 +54,7 @@ struct Layout {
     int planes;
 };
 
-Layout auto_layout(uint64_t rows, const gol_config* cfg, bool composite_part = false)
+Layout auto_layout(uint64_t rows, const gol_config* cfg)
 {
     const bool fixed = (cfg->birth_mask == GOL_REF_BIRTH && cfg->survive_mask == GOL_REF_SURVIVE) ||
                        (cfg->birth_mask == GOL_CONWAY_BIRTH &&
@@ -66,11 +65,6 @@ Layout auto_layout(uint64_t rows, const gol_config* cfg, bool composite_part = f
         l.K = cfg->tb_depth;
     } else if (cfg->word_planes == 4) {
         l.K = 8;
-    } else if (cfg->word_planes == 0 && fixed && deflt_var &&
-               rows >= (composite_part ? 32768u : 65536u)) {
-        l.K = 8;
-        l.planes = 4;
-        return l;
     } else if (rows <= 6144) {
         l.K = 8;
     } else if (cfg->kernel_variant == 2 || !fixed) {
@@ -653,7 +647,7 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
         // composite: S same-device stripes with deep halos, advanced together
         gol_config c = *cfg;
         c.streams = 1;
-        const Layout lay = auto_layout(h / S, cfg, true);
+        const Layout lay = auto_layout(h / S, cfg);
         c.tb_depth = lay.K;
         c.word_planes = (uint32_t)lay.planes;
         if (!c.halo_depth) c.halo_depth = 16 * c.tb_depth;
