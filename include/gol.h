@@ -41,7 +41,8 @@ typedef enum gol_status {
     GOL_EHIP = 3,   /* HIP runtime error */
     GOL_ERCCL = 4,  /* RCCL error */
     GOL_EIO = 5,    /* file I/O error (CLI helpers) */
-    GOL_ESTATE = 6  /* call not valid in the engine's current state */
+    GOL_ESTATE = 6, /* call not valid in the engine's current state */
+    GOL_EXFER = 7   /* halo transport callback failed (gol_create_rank_transport) */
 } gol_status;
 
 typedef enum gol_semantics {
@@ -68,18 +69,16 @@ typedef struct gol_config {
     uint32_t semantics;    /* gol_semantics */
     uint32_t ref_ranks;    /* P for GOL_SEM_REF_STRIPES (must satisfy h >= P) */
     uint32_t tb_depth;     /* generations fused per kernel launch (temporal
-                              blocking); 0 = auto; allowed 1,2,4,6,7,8,12,16,
-                              20,24,32 */
+                              blocking); 0 = auto; allowed 1,2,4,6,7,8,12,16
+                              (the dev build, make dev, adds 20,24,32) */
     uint32_t halo_depth;   /* multi-rank: halo rows exchanged per round
                               (= generations between exchanges); 0 = auto */
     uint32_t rows_per_wave;/* rows each wavefront streams per launch; 0 = auto */
-    uint32_t kernel_variant;/* stencil kernel: 0 = auto (= 1); 1 = total-sum
-                              state (9-cell sums, 10 VGPRs per fused
-                              generation and plane pair), anti-diagonal
-                              schedule; 2 = neighbour-sum state (14 VGPRs, +4
-                              VALU ops per word-generation, tb_depth <= 16,
-                              <= 8 with word_planes 4); 3 = as 1 with a
-                              step-major schedule (for A/B measurements) */
+    uint32_t handoff;      /* row blocks of a launch: 0 = auto (= on), 1 = off
+                              (every block recomputes the K(K-1) stage-steps of
+                              its vertical halo), 2 = on (each block takes the
+                              rows it needs beyond its own from the block below,
+                              which computed them first; tb_depth >= 4) */
     uint32_t streams;      /* gol_create, GLOBAL only: split the field into this
                               many row stripes advanced on their own streams of
                               the device (k-deep halos, device copies), so one
@@ -88,11 +87,9 @@ typedef struct gol_config {
     uint32_t strip_lanes;  /* lanes per column strip of the stencil kernel: 64, 32
                               or 16 (2 of them halo, 64/L strips per wavefront);
                               0 = auto (narrow strips for short stripes) */
-    uint32_t word_planes;  /* cell planes per lane of the stencil kernel: 2 (one
-                              word = 64 columns per lane, every tb_depth) or 4
-                              (two words = 128 columns per lane: half the lane
-                              moves and funnel shifts per cell; tb_depth <= 16);
-                              0 = auto (= 2; 4 only on request) */
+    uint32_t word_planes;  /* cell planes per lane: 0 = auto (= 2: one word = 64
+                              columns per lane); 4 (two words per lane) exists
+                              only in the dev build (make dev) */
 } gol_config;
 
 typedef struct gol_engine gol_engine;
@@ -164,6 +161,10 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0,
 gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave,
                          uint32_t* word_planes);
 
+/* Whether full-depth launches use hand-off row blocks (gol_config.handoff, as
+ * the planner resolved it): 1 = yes, 0 = every block recomputes its halo. */
+gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff);
+
 /* ---- Multi-GPU, one process per GPU (replaces the MPI stripes :70-81 and the
  * halo exchange :104-145 with RCCL send/recv over xGMI) ---- */
 
@@ -179,6 +180,51 @@ gol_status gol_comm_unique_id(uint8_t id[128]);
  * it collectively with the same id.  cfg->semantics must be GLOBAL. */
 gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int rank,
                            int nranks, const uint8_t id[128], gol_engine** out);
+
+/* Halo transport supplied by the caller (host memory): the same rank engine,
+ * partition and rounds as gol_create_rank, but each exchange stages the Hx
+ * boundary rows through host buffers and calls `exchange`, which must send
+ * send_up to rank-1 and send_down to rank+1 and receive recv_up from rank-1 and
+ * recv_down from rank+1, `bytes` each (NULL pointers where there is no such
+ * neighbour), and return 0 on success.  This is the reference's own transport
+ * shape (MPI_Sendrecv of boundary rows, Parallel_Life_MPI.cpp:104-145, here with
+ * the receive landing in the halo); gol-mpi --transport mpi uses it, and it lets
+ * several ranks share one GPU, which RCCL refuses. */
+typedef int (*gol_halo_exchange_fn)(void* ctx, const void* send_up, void* recv_up,
+                                    const void* send_down, void* recv_down, uint64_t bytes);
+typedef struct gol_transport {
+    gol_halo_exchange_fn exchange;
+    void* ctx;
+} gol_transport;
+gol_status gol_create_rank_transport(uint64_t h, uint64_t w, const gol_config* cfg, int rank,
+                                     int nranks, const gol_transport* transport,
+                                     gol_engine** out);
+
+/* The launch/exchange schedule a rank engine (or group member) runs for one
+ * gol_step(generations) call -- host-only, no GPU needed; gol_step executes
+ * exactly this list.  halo_fresh: the previous call ended with an overlapped
+ * exchange still to be waited for (0 after create/load).  Launch ops name the
+ * local buffer rows they write (local row i = field row row0 - Hx + i). */
+typedef enum gol_sched_kind {
+    GOL_OP_EXCHANGE = 0,       /* blocking halo exchange on the compute stream */
+    GOL_OP_WAIT_EXCHANGE = 1,  /* compute waits for the overlapped exchange */
+    GOL_OP_LAUNCH = 2,         /* stencil launch over the valid region */
+    GOL_OP_BAND = 3,           /* last launch of a round, boundary rows only */
+    GOL_OP_INTERIOR = 4,       /* ... and the rest of the own rows, concurrently */
+    GOL_OP_EXCHANGE_ASYNC = 5  /* exchange of the band rows, overlapping INTERIOR */
+} gol_sched_kind;
+typedef struct gol_sched_op {
+    uint32_t kind;      /* gol_sched_kind */
+    uint32_t depth;     /* fused generations of a launch (0 otherwise) */
+    uint32_t shrink;    /* halo rows consumed per side once this launch is done */
+    uint32_t nseg;      /* output row ranges of a launch: [out_lo[i], out_hi[i]) */
+    int64_t out_lo[2];
+    int64_t out_hi[2];
+} gol_sched_op;
+gol_status gol_round_schedule(uint64_t h, uint64_t w, const gol_config* cfg, int rank,
+                              int nranks, uint64_t generations, int halo_fresh,
+                              gol_sched_op* ops, uint64_t cap, uint64_t* nops,
+                              uint32_t* tb_depth, uint32_t* halo_depth);
 
 /* ---- Multi-GPU (or multi-stripe) inside ONE process, no RCCL ----
  * `nranks` stripe engines of one GLOBAL field (the same partition and halo

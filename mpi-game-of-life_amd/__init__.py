@@ -16,7 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOL_LIB") or os.path.join(HERE, "libgol.so")
 CLI_PATH = os.path.join(HERE, "gol")
 
-GOL_OK, GOL_EINVAL, GOL_ENOMEM, GOL_EHIP, GOL_ERCCL, GOL_EIO, GOL_ESTATE = range(7)
+GOL_OK, GOL_EINVAL, GOL_ENOMEM, GOL_EHIP, GOL_ERCCL, GOL_EIO, GOL_ESTATE, GOL_EXFER = range(8)
+# gol_sched_kind (include/gol.h)
+OP_EXCHANGE, OP_WAIT_EXCHANGE, OP_LAUNCH, OP_BAND, OP_INTERIOR, OP_EXCHANGE_ASYNC = range(6)
+OP_NAMES = ["EXCHANGE", "WAIT_EXCHANGE", "LAUNCH", "BAND", "INTERIOR", "EXCHANGE_ASYNC"]
 SEM_GLOBAL, SEM_REF_STRIPES = 0, 1
 
 # (birth, survive) masks; bit n <=> n live neighbours
@@ -30,6 +33,7 @@ EXPORTS = [
     "gol_digest", "gol_destroy", "gol_last_error", "gol_set_timing", "gol_get_timing",
     "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
     "gol_create_rank", "gol_create_group", "gol_group_step", "gol_plan_info",
+    "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
 ]
 
 
@@ -49,7 +53,7 @@ class Config(ctypes.Structure):
         ("tb_depth", ctypes.c_uint32),
         ("halo_depth", ctypes.c_uint32),
         ("rows_per_wave", ctypes.c_uint32),
-        ("kernel_variant", ctypes.c_uint32),
+        ("handoff", ctypes.c_uint32),
         ("streams", ctypes.c_uint32),
         ("strip_lanes", ctypes.c_uint32),
         ("word_planes", ctypes.c_uint32),
@@ -67,9 +71,30 @@ class Timing(ctypes.Structure):
     ]
 
 
+class SchedOp(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_uint32),
+        ("depth", ctypes.c_uint32),
+        ("shrink", ctypes.c_uint32),
+        ("nseg", ctypes.c_uint32),
+        ("out_lo", ctypes.c_int64 * 2),
+        ("out_hi", ctypes.c_int64 * 2),
+    ]
+
+
+# gol_halo_exchange_fn(ctx, send_up, recv_up, send_down, recv_down, bytes) -> int
+HALO_EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_uint64)
+
+
+class Transport(ctypes.Structure):
+    _fields_ = [("exchange", HALO_EXCHANGE_FN), ("ctx", ctypes.c_void_p)]
+
+
 def build(force=False):
     """Compile libgol.so and the CLI in-tree (hipcc --offload-arch=gfx950)."""
-    args = ["make", "-s", "-C", HERE, "-j4"]
+    args = ["make", "-s", "-C", HERE, "-j8"]
     if force:
         subprocess.run(["make", "-s", "-C", HERE, "clean"], check=True)
     subprocess.run(args, check=True)
@@ -120,11 +145,18 @@ def lib():
                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp)]
     L.gol_group_step.argtypes = [ctypes.POINTER(vp), i32, u64]
     L.gol_plan_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    L.gol_plan_handoff.argtypes = [vp, ctypes.POINTER(u32)]
+    L.gol_create_rank_transport.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32,
+                                            ctypes.POINTER(Transport), ctypes.POINTER(vp)]
+    L.gol_round_schedule.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32, u64, i32,
+                                     ctypes.POINTER(SchedOp), u64, pu64, ctypes.POINTER(u32),
+                                     ctypes.POINTER(u32)]
     for name in ["gol_create", "gol_create_rank", "gol_load_ascii", "gol_store_ascii",
                  "gol_load_packed", "gol_store_packed", "gol_init_random", "gol_step",
                  "gol_sync", "gol_digest", "gol_set_timing", "gol_get_timing",
                  "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
-                 "gol_create_group", "gol_group_step", "gol_plan_info"]:
+                 "gol_create_group", "gol_group_step", "gol_plan_info", "gol_plan_handoff",
+                 "gol_create_rank_transport", "gol_round_schedule"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -136,7 +168,7 @@ def _check(st):
 
 
 def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_depth=0,
-                halo_depth=0, rows_per_wave=0, kernel_variant=0, streams=0, strip_lanes=0,
+                halo_depth=0, rows_per_wave=0, handoff=0, streams=0, strip_lanes=0,
                 word_planes=0):
     c = Config()
     lib().gol_config_init(ctypes.byref(c))
@@ -147,7 +179,7 @@ def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_
     c.tb_depth = tb_depth
     c.halo_depth = halo_depth
     c.rows_per_wave = rows_per_wave
-    c.kernel_variant = kernel_variant
+    c.handoff = handoff
     c.streams = streams
     c.strip_lanes = strip_lanes
     c.word_planes = word_planes
@@ -158,6 +190,25 @@ def rank_rows(h, nranks, rank):
     r0, n = ctypes.c_uint64(), ctypes.c_uint64()
     _check(lib().gol_rank_rows(h, nranks, rank, ctypes.byref(r0), ctypes.byref(n)))
     return r0.value, n.value
+
+
+def round_schedule(h, w, rank, nranks, gens, halo_fresh=False, **cfg_kw):
+    """The launch/exchange schedule gol_step runs on stripe `rank` of `nranks`
+    (gol_round_schedule; host-only).  Returns (ops, K, Hx), ops as dicts with
+    kind (OP_*), depth, shrink and segs [(out_lo, out_hi), ...] in local rows."""
+    cfg = make_config(**cfg_kw)
+    n, K, Hx = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().gol_round_schedule(h, w, ctypes.byref(cfg), rank, nranks, gens,
+                                    1 if halo_fresh else 0, None, 0, ctypes.byref(n),
+                                    ctypes.byref(K), ctypes.byref(Hx)))
+    arr = (SchedOp * max(1, n.value))()
+    _check(lib().gol_round_schedule(h, w, ctypes.byref(cfg), rank, nranks, gens,
+                                    1 if halo_fresh else 0, arr, n.value, ctypes.byref(n),
+                                    ctypes.byref(K), ctypes.byref(Hx)))
+    ops = [{"kind": o.kind, "depth": o.depth, "shrink": o.shrink,
+            "segs": [(o.out_lo[i], o.out_hi[i]) for i in range(o.nseg)]}
+           for o in arr[:n.value]]
+    return ops, K.value, Hx.value
 
 
 def unique_id() -> bytes:
@@ -171,16 +222,26 @@ class Engine:
 
     def __init__(self, h, w, rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1,
                  tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None,
-                 kernel_variant=0, streams=0, strip_lanes=0, word_planes=0, _handle=None):
+                 handoff=0, streams=0, strip_lanes=0, word_planes=0, transport=None,
+                 _handle=None):
+        """transport: for a rank engine, a callable (send_up, send_down) -> (recv_up,
+        recv_down) of bytes objects (None where there is no neighbour) used instead
+        of RCCL (gol_create_rank_transport)."""
         self.h, self.w = h, w
         self.wq = (w + 63) // 64
+        self._tp = None
         cfg = make_config(rule, device, semantics, ref_ranks, tb_depth, halo_depth,
-                          rows_per_wave, kernel_variant, streams, strip_lanes, word_planes)
+                          rows_per_wave, handoff, streams, strip_lanes, word_planes)
         handle = ctypes.c_void_p()
         if _handle is not None:
             handle = _handle
         elif rank is None:
             _check(lib().gol_create(h, w, ctypes.byref(cfg), ctypes.byref(handle)))
+        elif transport is not None:
+            self._tp = _make_transport(transport)
+            _check(lib().gol_create_rank_transport(h, w, ctypes.byref(cfg), rank, nranks,
+                                                   ctypes.byref(self._tp[0]),
+                                                   ctypes.byref(handle)))
         else:
             if uid is None or len(uid) != 128:
                 raise GolError(GOL_EINVAL, "rank engines need a 128-byte RCCL unique id")
@@ -198,6 +259,9 @@ class Engine:
         _check(lib().gol_plan_info(self._h, ctypes.byref(sl), ctypes.byref(rp), ctypes.byref(wp)))
         self.strip_lanes = sl.value
         self.word_planes = wp.value
+        ho = ctypes.c_uint32()
+        _check(lib().gol_plan_handoff(self._h, ctypes.byref(ho)))
+        self.handoff = bool(ho.value)
 
     def close(self):
         if self._h:
@@ -265,16 +329,38 @@ class Engine:
                 "cell_gens_computed": t.cell_gens_computed, "streams": t.streams}
 
 
+def _make_transport(fn):
+    """Wrap a Python halo exchange `fn(send_up, send_down) -> (recv_up, recv_down)`
+    (bytes or None) as a gol_transport; keep the result alive with the engine."""
+    def cb(ctx, send_up, recv_up, send_dn, recv_dn, nbytes):
+        try:
+            su = ctypes.string_at(send_up, nbytes) if send_up else None
+            sd = ctypes.string_at(send_dn, nbytes) if send_dn else None
+            ru, rd = fn(su, sd)
+            for ptr, data in ((recv_up, ru), (recv_dn, rd)):
+                if ptr:
+                    if data is None or len(data) != nbytes:
+                        return 2
+                    ctypes.memmove(ptr, data, nbytes)
+            return 0
+        except Exception:  # a Python error must not unwind through C
+            import traceback
+            traceback.print_exc()
+            return 1
+    cfn = HALO_EXCHANGE_FN(cb)
+    return Transport(cfn, None), cfn
+
+
 class Group:
     """`nranks` stripe engines of one field in this process (gol_create_group):
     the multi-GPU partition/halo logic with device-copy transport; stripes may
     share a GPU."""
 
     def __init__(self, h, w, nranks, devices=None, rule=REF_RULE, tb_depth=0, halo_depth=0,
-                 rows_per_wave=0, kernel_variant=0, strip_lanes=0, word_planes=0):
+                 rows_per_wave=0, handoff=0, strip_lanes=0, word_planes=0):
         self.h, self.w, self.n = h, w, nranks
         cfg = make_config(rule, -1 if devices else 0, SEM_GLOBAL, 1, tb_depth, halo_depth,
-                          rows_per_wave, kernel_variant, strip_lanes=strip_lanes,
+                          rows_per_wave, handoff, strip_lanes=strip_lanes,
                           word_planes=word_planes)
         hs = (ctypes.c_void_p * nranks)()
         devs = (ctypes.c_int * nranks)(*(devices or [0] * nranks))

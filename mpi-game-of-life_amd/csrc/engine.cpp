@@ -1,6 +1,7 @@
 // engine.cpp -- host side of libgol.so: the C ABI of include/gol.h.
 //
-// Owns device memory, the HIP stream, the RCCL communicator and the launch
+// Owns device memory, the HIP streams, the halo transport (RCCL communicator,
+// a caller's host transport, or device copies inside a group) and the launch
 // plans.  Mirrors main()'s flow in Parallel_Life_MPI.cpp:190-240: create
 // (readGridFromFile's allocation :88-89) -> load (:91-99) -> step (the epoch loop
 // :215-221 with the halo exchange :104-145) -> store (:157-164).
@@ -8,9 +9,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
-#include <map>
+#include <climits>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -29,26 +31,19 @@ thread_local std::string g_last_error;
 // stripes on 2 streams (measured +11% at 65536^2; no gain at <= 16384 rows,
 // profiles/r01/group_bench_*.jsonl)
 constexpr uint64_t kCompositeMinRows = 32768;
+// captured step graphs kept per engine (least recently used evicted)
+constexpr size_t kGraphCache = 8;
 
 // Auto launch layout: fused depth K and planes per lane group (bitlayout.h).
-//  * 2 planes (one word per lane), K = 16 (202 VGPRs, 2 waves/SIMD, enough for
-//    full VALU issue) for stripes of more than 6144 rows: 124.5 TCUPS at 65536^2
-//    vs 122.4 (K = 8, 4 waves/SIMD) and 106.0 (K = 12), 92 vs 80 / 79 at
-//    8192x65536; K >= 20 drops to 1 wave/SIMD (half issue rate) and loses 30-35%
-//    (profiles/r01/sweep_total_sum_depth.jsonl).
-//  * 4 planes (two words per lane: 17% fewer VALU issue slots per cell, but K = 8
-//    to keep 2 waves/SIMD at 236 VGPRs) only when asked for (word_planes = 4).
-//    Once the 2-plane K = 16 kernel got its 8-step prefetch ring it wins
-//    everywhere: 129.1 vs 123.7 TCUPS at 65536^2 (composite, in-process A/B,
-//    profiles/r01/ab_default_layout_pf8.jsonl), and it was already ahead on lone
-//    stripes of 33024 rows or fewer (profiles/r01/ab_word_planes_r01.jsonl,
-//    sweep_word_planes.jsonl).
-//  * Short fields are launch-latency bound and keep K = 8 with 2 planes (4096^2:
-//    11.0-11.6 TCUPS vs 8.7 at K = 16 and 8.1 with 4 planes).
+//  * K = 16 with 2 planes (one word per lane; ~230 VGPRs, 2 waves/SIMD, enough
+//    for full VALU issue) for stripes of more than 6144 rows: 124.5 TCUPS at
+//    65536^2 vs 122.4 (K = 8) and 106.0 (K = 12); K >= 20 drops to 1 wave/SIMD
+//    and loses 30-35% (profiles/r01/sweep_total_sum_depth.jsonl).
+//  * Short fields are launch-latency bound and keep K = 8 (4096^2: 11.0-11.6
+//    TCUPS vs 8.7 at K = 16).
 //  * Rules other than B/S2 and B3/S23 evaluate a 10-term mask sum whose K = 16
 //    state spills: K = 12.
-// Explicit tb_depth / word_planes / kernel_variant settings are kept; a missing
-// one is filled in to match (4 planes only with depth <= 16).
+//  * 4 planes (two words per lane) only on request (dev build), with K = 8.
 struct Layout {
     uint32_t K;
     int planes;
@@ -59,19 +54,13 @@ Layout auto_layout(uint64_t rows, const gol_config* cfg)
     const bool fixed = (cfg->birth_mask == GOL_REF_BIRTH && cfg->survive_mask == GOL_REF_SURVIVE) ||
                        (cfg->birth_mask == GOL_CONWAY_BIRTH &&
                         cfg->survive_mask == GOL_CONWAY_SURVIVE);
-    const bool deflt_var = cfg->kernel_variant == 0 || cfg->kernel_variant == 1;
     Layout l;
-    if (cfg->tb_depth) {
+    if (cfg->tb_depth)
         l.K = cfg->tb_depth;
-    } else if (cfg->word_planes == 4) {
+    else if (cfg->word_planes == 4 || rows <= 6144)
         l.K = 8;
-    } else if (rows <= 6144) {
-        l.K = 8;
-    } else if (cfg->kernel_variant == 2 || !fixed) {
-        l.K = 12;  // neighbour-sum state (14 VGPRs per stage) / generic rules
-    } else {
-        l.K = 16;
-    }
+    else
+        l.K = fixed ? 16 : 12;
     l.planes = cfg->word_planes ? (int)cfg->word_planes : 2;
     return l;
 }
@@ -97,6 +86,11 @@ gol_status fail(gol_status st, const std::string& msg)
             return fail(GOL_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(_r));     \
     } while (0)
 
+#define GOL_TRY(expr)                                                                       \
+    do {                                                                                    \
+        gol_status _s = (expr);                                                             \
+        if (_s != GOL_OK) return _s;                                                        \
+    } while (0)
 
 uint64_t last_mask(uint64_t w)
 {
@@ -135,7 +129,26 @@ struct Region {
     uint64_t buf_row, glob_row, user_row, rows;
 };
 
+// Geometry of stripe `rank` of `nranks` (GLOBAL field), host-only: its rows, the
+// halo depth, the fused depth, and the segment tables of its launch plans --
+// plans[c-1] computes the local rows still valid after a cumulative shrink c of a
+// round (c = 1..Hx); with overlap, plans[Hx] (band: the rows the neighbours need)
+// and plans[Hx+1] (interior) split the round's last launch.  Shared by the rank
+// engines and gol_round_schedule, so the exported schedule is the one run.
+struct RankGeom {
+    uint64_t row0 = 0, R = 0, Hx = 0, buf_rows = 0;
+    uint32_t K = 8;
+    bool overlap = false;
+    std::vector<std::vector<SegDesc>> raw;
+};
+
+gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks, RankGeom* g);
+
 }  // namespace
+
+// The kinds of exchange a stripe engine does (gol_create_rank /
+// gol_create_rank_transport / gol_create_group).
+enum XferKind { XFER_NONE = 0, XFER_RCCL = 1, XFER_HOST = 2, XFER_GROUP = 3 };
 
 struct gol_engine {
     int device = 0;
@@ -149,14 +162,17 @@ struct gol_engine {
     uint32_t K = 8;
     uint32_t rows_per_wave = 0;
     int lane_shift = -1;  // strip width 64 >> lane_shift; -1 = chosen per plan
-    int var = 0;  // stencil kernel variant (life_internal.h launch_life)
+    uint32_t handoff = 0; // gol_config.handoff
     uint32_t sem = GOL_SEM_GLOBAL;
     uint32_t P = 1;
 
     // rank geometry (single-GPU: rank 0 of 1, Hx = 0)
     int rank = 0, nranks = 1;
     uint64_t row0 = 0, R = 0, Hx = 0;
+    XferKind xfer = XFER_NONE;
     ncclComm_t comm = nullptr;
+    gol_transport tp{nullptr, nullptr};
+    uint64_t* host_xfer = nullptr;  // pinned: send_up | recv_up | send_dn | recv_dn
 
     // in-process group (gol_create_group): halo exchange by device copies
     gol_engine* up = nullptr;
@@ -166,14 +182,13 @@ struct gol_engine {
 
     // exchange/compute overlap (multi-rank): the last launch of a full round is
     // split into a band launch (the rows the neighbours need) and an interior
-    // launch; the exchange runs on `comm` between them.  plans[Hx] = band,
-    // plans[Hx+1] = interior.  halo_fresh: the current buffer's halo rows were
-    // already exchanged (completion signalled by ev_xdone on `comm`).
-    // The band launch runs on its own stream, concurrently with the interior
-    // launch: it is a few hundred rows, far too few wavefronts to fill the GPU,
-    // so serialising it before the interior would leave the chip mostly idle.
+    // launch; the exchange runs on `comm_stream` between them.  halo_fresh: the
+    // current buffer's halo rows were already exchanged (completion signalled by
+    // ev_xdone on comm_stream).  The band launch runs on its own stream,
+    // concurrently with the interior launch: it is a few hundred rows, far too
+    // few wavefronts to fill the GPU.
     hipStream_t comm_stream = nullptr, band_stream = nullptr;
-    hipEvent_t ev_band = nullptr, ev_xdone = nullptr, ev_in = nullptr;
+    hipEvent_t ev_band = nullptr, ev_xdone = nullptr, ev_in = nullptr, ev_join = nullptr;
     bool overlap = false;
     bool halo_fresh = false;
 
@@ -195,9 +210,17 @@ struct gol_engine {
         double own_rows = 0;  // output rows of this plan that are the caller's rows
         int64_t rpw = 0;      // rows per wavefront
         int64_t total_units = 0;
+        bool multi_blk = false;  // some segment has more than one row block
+        bool hand = false;       // the planner chose hand-off row blocks
         SegDesc* dev = nullptr;
     };
-    std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: plans[c-1] for shrink c
+    std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: see RankGeom
+
+    // row-block hand-off buffers (life_stencil.h): region 0 serves launches on
+    // `stream`, region 1 those on `band_stream` (the two may run concurrently)
+    uint64_t* side[2] = {nullptr, nullptr};
+    uint32_t* flags[2] = {nullptr, nullptr};
+    int* d_err = nullptr;
 
     std::vector<Region> user_regions;  // load/store mapping (own output rows)
     std::vector<Region> load_regions;  // rows loaded (REF_STRIPES loads overlaps too)
@@ -208,7 +231,13 @@ struct gol_engine {
     // single-stream engines replay a captured hipGraph of the launch sequence of a
     // gol_step(gens) call (keyed by gens and the starting buffer), so a step of
     // many short launches costs one graph launch of host work
-    std::map<std::pair<uint64_t, int>, std::pair<hipGraphExec_t, int>> graphs;
+    struct GraphEntry {
+        hipGraphExec_t exec;
+        int cur_after;
+        uint64_t used;
+    };
+    std::map<std::pair<uint64_t, int>, GraphEntry> graphs;
+    uint64_t graph_clock = 0;
 
     // timing: HIP events around every `timing_every`-th stencil launch (0 = off)
     uint32_t timing_every = 0;
@@ -248,72 +277,113 @@ int32_t strip_groups(uint64_t wq, int shift)
     return (int32_t)((strips + per - 1) / per);
 }
 
+// Hand-off constraints on the rows per wavefront R of a launch of depth d: a
+// consumer streams R + 2 input rows in whole prefetch blocks after the warm-up
+// blocks (life_stencil.h), so R + 2 is a multiple of the prefetch block and
+// R + 2 >= warm-up + one block.
+bool handoff_fits(int64_t R, int d, int planes)
+{
+    if (d < gol::kHandoffMinDepth) return false;
+    const int pf = gol::prefetch_of(d, planes);
+    return (R + 2) % pf == 0 && R + 2 >= gol::warm_steps_of(d, planes) + pf;
+}
+
 // Rows per wavefront and strip width for one launch plan.  Every wavefront of
-// a launch does the same work, (R + K + 1) stage-steps of K stages (R output
-// rows, K+1 rows of warm-up/halo), so the launch time is set by the most loaded
-// SIMD: n = ceil(units / SIMDs) wavefronts run in rounds of `occ` resident ones,
-// and a partial round of m wavefronts still costs max(2, m) issue slots per
-// instruction (one wavefront alone issues at half the SIMD's VALU rate).
-// Measured (profiles/r01/sweep_rows_per_wave*.jsonl): keeping fewer than `occ`
-// wavefronts per SIMD all launch long is 5-10% slower than the model says, so
-// R is restricted to n >= occ whenever the field is large enough.  Narrower
-// strips (32 or 16 lanes, 2 or 4 per wavefront) multiply the units per row
-// block, so short stripes reach `occ` with longer row blocks; the model picks
-// the cheapest (strip width, R).
+// a launch does about the same work, so the launch time is set by the most
+// loaded SIMD: n = ceil(units / SIMDs) wavefronts run in rounds of `occ`
+// resident ones, and a partial round of m wavefronts still costs max(2, m) issue
+// slots per instruction (one wavefront alone issues at half the SIMD's VALU rate).
+// A wavefront's work in rows of K stage-steps: classic blocks R + K + 1 (+ c0
+// fixed), hand-off blocks R + 2 (+ c0 + the hand-off's own cost).  Measured
+// (profiles/r01/sweep_rows_per_wave*.jsonl): keeping fewer than `occ`
+// wavefronts per SIMD all launch long is 5-10% slower than the model says, so R
+// is restricted to n >= occ whenever the field is large enough.  Narrower strips
+// (32 or 16 lanes, 2 or 4 per wavefront) multiply the units per row block, so
+// short stripes reach `occ` with longer row blocks.
 struct RowPlan {
     int64_t rpw;
     int32_t groups, lane_shift;
+    bool hand;
 };
 
-RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K, int occ,
-                           int simds, int force_rpw, int force_shift)
+RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K, int planes,
+                           int occ_classic, int occ_hand, int simds, int force_rpw,
+                           int force_shift, uint32_t handoff)
 {
-    const int64_t c0 = 3;  // per-wavefront fixed cost, in rows
+    const int64_t c0 = 3;      // per-wavefront fixed cost, in rows
+    const int64_t c_hand = 2;  // side-row stores, flag wait, shorter tail ILP
     int64_t maxrows = 1;
     for (const auto& s : segs) maxrows = std::max<int64_t>(maxrows, s.out_hi - s.out_lo);
-    RowPlan best_p[2] = {{16, strip_groups(wq, 0), 0}, {16, strip_groups(wq, 0), 0}};
-    double best[2] = {1e300, 1e300};
-    for (int shift = 0; shift <= 2; ++shift) {
-        if (force_shift >= 0 && shift != force_shift) continue;
-        const int32_t groups = strip_groups(wq, shift);
-        const int64_t r_lo = force_rpw ? force_rpw : std::max<int64_t>(8, K + 2);
-        const int64_t r_hi =
-            force_rpw ? force_rpw : std::max<int64_t>(r_lo, std::min<int64_t>(1024, maxrows + K));
-        for (int64_t R = r_lo; R <= r_hi; ++R) {
-            int64_t units = 0;
-            for (const auto& sg : segs)
-                units += groups * ((std::max<int64_t>(0, sg.out_hi - sg.out_lo) + R - 1) / R);
-            const int64_t n = (units + simds - 1) / simds;
-            const int64_t full = n / occ, rem = n % occ;
-            const double slots =
-                (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
-            const double cost = slots * (double)(R + K + 1 + c0);
-            const int filled = n >= occ ? 1 : 0;
-            if (cost < best[filled] * 0.999) {
-                best[filled] = cost;
-                best_p[filled] = {R, groups, shift};
+    // best [hand][filled]: filled = at least `occ` wavefronts per SIMD
+    RowPlan best_p[2][2];
+    double best[2][2] = {{1e300, 1e300}, {1e300, 1e300}};
+    for (int hand = 0; hand <= 1; ++hand) {
+        best_p[hand][0] = best_p[hand][1] = {16, strip_groups(wq, 0), 0, hand != 0};
+        if (hand && (handoff == 1 || K < gol::kHandoffMinDepth)) continue;
+        const int occ = std::max(1, hand ? occ_hand : occ_classic);
+        for (int shift = 0; shift <= 2; ++shift) {
+            if (force_shift >= 0 && shift != force_shift) continue;
+            const int32_t groups = strip_groups(wq, shift);
+            const int64_t r_lo = force_rpw ? force_rpw : std::max<int64_t>(8, K + 2);
+            const int64_t r_hi =
+                force_rpw ? force_rpw : std::max<int64_t>(r_lo, std::min<int64_t>(1024, maxrows + K));
+            for (int64_t R = r_lo; R <= r_hi; ++R) {
+                if (hand && !handoff_fits(R, K, planes)) continue;
+                int64_t units = 0, blocks_max = 0;
+                for (const auto& sg : segs) {
+                    const int64_t nb = (std::max<int64_t>(0, sg.out_hi - sg.out_lo) + R - 1) / R;
+                    units += groups * nb;
+                    blocks_max = std::max(blocks_max, nb);
+                }
+                if (hand && blocks_max < 2) continue;  // nothing to hand over
+                const int64_t n = (units + simds - 1) / simds;
+                const int64_t full = n / occ, rem = n % occ;
+                const double slots =
+                    (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
+                const double rows = hand ? (double)(R + 2 + c0 + c_hand) : (double)(R + K + 1 + c0);
+                const double cost = slots * rows;
+                const int filled = n >= occ ? 1 : 0;
+                if (cost < best[hand][filled] * 0.999) {
+                    best[hand][filled] = cost;
+                    best_p[hand][filled] = {R, groups, shift, hand != 0};
+                }
             }
         }
     }
-    return best[1] < 1e300 ? best_p[1] : best_p[0];
+    // per kind: a plan that fills the SIMDs if there is one
+    const int fc = best[0][1] < 1e300 ? 1 : 0, fh = best[1][1] < 1e300 ? 1 : 0;
+    const bool have_hand = best[1][fh] < 1e300;
+    if (handoff == 2 && have_hand) return best_p[1][fh];
+    if (handoff == 1 || !have_hand) return best_p[0][fc];
+    // auto: the cheaper, preferring plans that fill the SIMDs
+    if (fh != fc) return fh > fc ? best_p[1][fh] : best_p[0][fc];
+    return best[1][fh] <= best[0][fc] ? best_p[1][fh] : best_p[0][fc];
 }
 
 gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
 {
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-    const int occ = std::max(1, gol::life_blocks_per_cu((int)e->K, e->rule, e->var, e->planes));
-    for (const auto& r : raw) {
+    const int occ_c = gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, false);
+    const int occ_h = e->K >= (uint32_t)gol::kHandoffMinDepth
+                          ? gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, true)
+                          : 0;
+    int64_t max_units = 0;
+    bool any_hand = false;
+    for (size_t pi = 0; pi < raw.size(); ++pi) {
+        const auto& r = raw[pi];
         gol_engine::Plan p;
         p.segs = r;
-        const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, occ, 4 * cus,
-                                              (int)e->rows_per_wave, e->lane_shift);
+        const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
+                                              (int)e->rows_per_wave, e->lane_shift, e->handoff);
         p.rpw = rp.rpw;
         p.groups = rp.groups;
         p.lane_shift = rp.lane_shift;
+        p.hand = rp.hand;
         finish_segs(p.segs, p.rpw, p.groups);
         p.total_units = plan_units(p.segs, p.groups);
         for (const auto& sg : p.segs) {
+            p.multi_blk |= sg.nblk > 1;
             // own rows of a segment: rank engines [Hx, Hx+R); REF_STRIPES the
             // rank's output rows; GLOBAL all rows
             int64_t olo = sg.out_lo, ohi = sg.out_hi;
@@ -330,10 +400,23 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
             }
             p.own_rows += (double)std::max<int64_t>(0, ohi - olo);
         }
+        max_units = std::max(max_units, p.total_units);
+        any_hand |= p.hand && p.multi_blk;
         HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * p.segs.size()));
         HIP_TRY(hipMemcpy(p.dev, p.segs.data(), sizeof(SegDesc) * p.segs.size(),
                           hipMemcpyHostToDevice));
         e->plans.push_back(p);
+    }
+    HIP_TRY(hipMalloc(&e->d_err, sizeof(int)));
+    HIP_TRY(hipMemset(e->d_err, 0, sizeof(int)));
+    if (any_hand && max_units > 0) {
+        const size_t slot = (size_t)2 * (e->K - 1) * 64 * (size_t)(e->planes / 2);
+        const int regions = e->overlap ? 2 : 1;
+        for (int r = 0; r < regions; ++r) {
+            HIP_TRY(hipMalloc(&e->side[r], (size_t)max_units * slot * sizeof(uint64_t)));
+            HIP_TRY(hipMalloc(&e->flags[r], (size_t)max_units * sizeof(uint32_t)));
+            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)max_units * sizeof(uint32_t)));
+        }
     }
     return GOL_OK;
 }
@@ -345,25 +428,144 @@ gol_status check_cfg(const gol_config* cfg)
         return fail(GOL_EINVAL, "rule masks must be 9-bit");
     if (cfg->tb_depth != 0 && std::find(std::begin(gol::kDepthList), std::end(gol::kDepthList),
                                         (int)cfg->tb_depth) == std::end(gol::kDepthList))
-        return fail(GOL_EINVAL, "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16,20,24,32");
-    if (cfg->kernel_variant > 3) return fail(GOL_EINVAL, "kernel_variant must be 0..3");
+        return fail(GOL_EINVAL, gol::kDevKernels
+                                    ? "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16,20,24,32"
+                                    : "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16 "
+                                      "(20/24/32: dev build)");
+    if (cfg->handoff > 2) return fail(GOL_EINVAL, "handoff must be 0 (auto), 1 (off) or 2 (on)");
+    if (cfg->handoff == 2 && cfg->tb_depth != 0 && cfg->tb_depth < (uint32_t)gol::kHandoffMinDepth)
+        return fail(GOL_EINVAL, "handoff on needs tb_depth >= 4");
     if (cfg->strip_lanes != 0 && cfg->strip_lanes != 64 && cfg->strip_lanes != 32 &&
         cfg->strip_lanes != 16)
         return fail(GOL_EINVAL, "strip_lanes must be 0 (auto), 64, 32 or 16");
-    if (cfg->kernel_variant == 2 && cfg->tb_depth > 16)
-        return fail(GOL_EINVAL, "kernel_variant 2 (neighbour-sum state) needs tb_depth <= 16");
     if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
     if (cfg->word_planes != 0 && cfg->word_planes != 2 && cfg->word_planes != 4)
         return fail(GOL_EINVAL, "word_planes must be 0 (auto), 2 or 4");
+    if (cfg->word_planes == 4 && !gol::kDevKernels)
+        return fail(GOL_EINVAL, "word_planes 4 is built only in the dev library (make dev)");
     if (cfg->word_planes == 4 && cfg->tb_depth > 16)
         return fail(GOL_EINVAL, "word_planes 4 needs tb_depth <= 16");
-    if (cfg->word_planes == 4 && cfg->kernel_variant == 2 && cfg->tb_depth > 8)
-        return fail(GOL_EINVAL, "word_planes 4 with kernel_variant 2 needs tb_depth <= 8");
     return GOL_OK;
 }
 
+gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks, RankGeom* g)
+{
+    gol_status st = gol_rank_rows(h, nranks, rank, &g->row0, &g->R);
+    if (st != GOL_OK) return st;
+    const uint64_t minR = h / (uint64_t)nranks;
+    if (minR == 0) return fail(GOL_EINVAL, "fewer rows than ranks");
+    g->K = auto_layout(g->R, cfg).K;
+    // rounds of halo_depth generations between exchanges (default 8 launches)
+    uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 8 * (uint64_t)g->K;
+    if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
+    g->Hx = nranks > 1 ? Hx : 0;
+    g->raw.clear();
+    g->overlap = false;
+    if (nranks <= 1) {
+        g->buf_rows = h;
+        return GOL_OK;
+    }
+    // local row i <-> field row row0 - Hx + i; buffer holds R + 2Hx rows
+    g->buf_rows = g->R + 2 * g->Hx;
+    const int64_t glob0 = (int64_t)g->row0 - (int64_t)g->Hx;
+    const int64_t in_field_lo = std::max<int64_t>(0, -glob0);
+    const int64_t in_field_hi = std::min<int64_t>((int64_t)g->buf_rows, (int64_t)h - glob0);
+    for (uint64_t c = 1; c <= g->Hx; ++c) {
+        SegDesc s{};
+        s.base_row = 0;
+        s.in_rows = (int64_t)g->buf_rows;
+        s.glob0 = glob0;
+        s.field_h = (int64_t)h;
+        s.out_lo = std::max<int64_t>((int64_t)c, in_field_lo);
+        s.out_hi = std::min<int64_t>((int64_t)(g->buf_rows - c), in_field_hi);
+        g->raw.push_back({s});
+    }
+    // overlap plans: rows neighbours need = own rows [Hx, 2Hx) (to rank-1) and
+    // [R, R+Hx) (to rank+1); interior = the rest of the own rows.  Decided from
+    // the smallest stripe so every rank / group member agrees (balanced stripes
+    // differ by one row).
+    const int64_t Hx_ = (int64_t)g->Hx, R = (int64_t)g->R;
+    if ((int64_t)(h / (uint64_t)nranks) >= 2 * Hx_) {
+        SegDesc b = g->raw.back()[0];  // shrink Hx: out = own rows
+        std::vector<SegDesc> band, inner;
+        int64_t ilo = Hx_, ihi = Hx_ + R;
+        if (rank > 0) {
+            SegDesc t = b;
+            t.out_lo = Hx_;
+            t.out_hi = 2 * Hx_;
+            band.push_back(t);
+            ilo = 2 * Hx_;
+        }
+        if (rank < nranks - 1) {
+            SegDesc t = b;
+            t.out_lo = R;
+            t.out_hi = R + Hx_;
+            band.push_back(t);
+            ihi = R;
+        }
+        SegDesc t = b;
+        t.out_lo = ilo;
+        t.out_hi = ihi;
+        inner.push_back(t);
+        g->raw.push_back(band);
+        g->raw.push_back(inner);
+        g->overlap = true;
+    }
+    return GOL_OK;
+}
+
+uint32_t pick_depth(uint32_t K, uint64_t remaining)
+{
+    for (int d : gol::kDepthList)
+        if ((uint32_t)d <= K && (uint64_t)d <= remaining) return (uint32_t)d;
+    return 1;
+}
+
+// One operation of a stripe engine's step (gol_sched_op without the rows).
+struct SchedOp {
+    uint32_t kind, depth;
+    int plan;  // launch ops: index into the plans (RankGeom)
+};
+
+// The launches of one round of `round` generations after a halo exchange: each
+// launch of depth d shrinks the valid region by d rows per side (plan c-1 for a
+// cumulative shrink of c).  With overlap, the last launch of a full round runs
+// as band + interior, with the next round's exchange started between them.
+void round_ops(uint32_t K, uint64_t Hx, bool overlap, uint64_t round, std::vector<SchedOp>& ops)
+{
+    uint64_t done = 0;
+    while (done < round) {
+        const uint32_t d = pick_depth(K, round - done);
+        done += d;
+        if (overlap && done == Hx) {
+            ops.push_back({GOL_OP_BAND, d, (int)Hx});
+            ops.push_back({GOL_OP_INTERIOR, d, (int)Hx + 1});
+            ops.push_back({GOL_OP_EXCHANGE_ASYNC, 0, -1});
+        } else {
+            ops.push_back({GOL_OP_LAUNCH, d, (int)(done - 1)});
+        }
+    }
+}
+
+// A stripe engine's gol_step(generations): rounds of Hx generations, each after
+// an exchange -- blocking, or the overlapped one the previous round started.
+void step_schedule(uint32_t K, uint64_t Hx, bool overlap, bool halo_fresh, uint64_t gens,
+                   std::vector<SchedOp>& ops)
+{
+    uint64_t left = gens;
+    while (left > 0) {
+        const uint64_t round = std::min<uint64_t>(left, Hx);
+        ops.push_back({halo_fresh ? (uint32_t)GOL_OP_WAIT_EXCHANGE : (uint32_t)GOL_OP_EXCHANGE, 0, -1});
+        const size_t n0 = ops.size();
+        round_ops(K, Hx, overlap, round, ops);
+        halo_fresh = ops.back().kind == GOL_OP_EXCHANGE_ASYNC && ops.size() > n0;
+        left -= round;
+    }
+}
+
 // Common construction; geometry (row0, R, Hx, rank) already set.
-gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* cfg)
+gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* cfg,
+                       const RankGeom* geom)
 {
     e->H = h;
     e->W = w;
@@ -383,10 +585,10 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
     e->rows_per_wave = cfg->rows_per_wave;
     e->lane_shift = cfg->strip_lanes == 64 ? 0 : cfg->strip_lanes == 32 ? 1
                   : cfg->strip_lanes == 16 ? 2 : -1;
-    e->var = cfg->kernel_variant == 2 ? 1 : cfg->kernel_variant == 3 ? 2 : 0;
+    e->handoff = cfg->handoff;
     e->planes = lay.planes;
-    if (!gol::life_has_kernel((int)e->K, e->var, e->planes))
-        return fail(GOL_EINVAL, "no stencil kernel for this tb_depth / kernel_variant / word_planes");
+    if (!gol::life_has_kernel((int)e->K, e->planes))
+        return fail(GOL_EINVAL, "no stencil kernel for this tb_depth / word_planes");
     {
         const uint64_t G = (uint64_t)e->planes / 2;
         e->ng = (e->wq + G - 1) / G;
@@ -408,57 +610,14 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         HIP_TRY(hipEventCreateWithFlags(&e->ev_band, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&e->ev_xdone, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
     }
 
     std::vector<std::vector<SegDesc>> raw;
     if (e->nranks > 1) {
-        // local row i <-> field row row0 - Hx + i; buffer holds R + 2Hx rows
-        e->buf_rows = e->R + 2 * e->Hx;
-        const int64_t glob0 = (int64_t)e->row0 - (int64_t)e->Hx;
-        const int64_t in_field_lo = std::max<int64_t>(0, -glob0);
-        const int64_t in_field_hi =
-            std::min<int64_t>((int64_t)e->buf_rows, (int64_t)h - glob0);
-        for (uint64_t c = 1; c <= e->Hx; ++c) {
-            SegDesc s{};
-            s.base_row = 0;
-            s.in_rows = (int64_t)e->buf_rows;
-            s.glob0 = glob0;
-            s.field_h = (int64_t)h;
-            s.out_lo = std::max<int64_t>((int64_t)c, in_field_lo);
-            s.out_hi = std::min<int64_t>((int64_t)(e->buf_rows - c), in_field_hi);
-            raw.push_back({s});
-        }
-        // overlap plans: rows neighbours need = own rows [Hx, 2Hx) (to rank-1) and
-        // [R, R+Hx) (to rank+1); interior = the rest of the own rows
-        // decided from the smallest stripe so every rank / group member agrees
-        // (balanced stripes differ by one row)
-        const int64_t Hx = (int64_t)e->Hx, R = (int64_t)e->R;
-        if ((int64_t)(h / (uint64_t)e->nranks) >= 2 * Hx) {
-            SegDesc b = raw.back()[0];  // shrink Hx: out = own rows
-            std::vector<SegDesc> band, inner;
-            int64_t ilo = Hx, ihi = Hx + R;
-            if (e->rank > 0) {
-                SegDesc t = b;
-                t.out_lo = Hx;
-                t.out_hi = 2 * Hx;
-                band.push_back(t);
-                ilo = 2 * Hx;
-            }
-            if (e->rank < e->nranks - 1) {
-                SegDesc t = b;
-                t.out_lo = R;
-                t.out_hi = R + Hx;
-                band.push_back(t);
-                ihi = R;
-            }
-            SegDesc t = b;
-            t.out_lo = ilo;
-            t.out_hi = ihi;
-            inner.push_back(t);
-            raw.push_back(band);
-            raw.push_back(inner);
-            e->overlap = true;
-        }
+        e->buf_rows = geom->buf_rows;
+        e->overlap = geom->overlap;
+        raw = geom->raw;
         e->user_regions.push_back({e->Hx, e->row0, 0, e->R});
         e->load_regions = e->user_regions;
     } else if (e->sem == GOL_SEM_REF_STRIPES) {
@@ -549,6 +708,7 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
                   hipStream_t stream = nullptr)
 {
     hipStream_t s = stream ? stream : e->stream;
+    const int region = (e->band_stream && s == e->band_stream) ? 1 : 0;
     const auto& p = e->plans[plan];
     StepArgs a{};
     a.in = e->buf[e->cur];
@@ -565,6 +725,14 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     a.total_units = p.total_units;
     a.birth = e->birth;
     a.survive = e->survive;
+    const bool hand = p.hand && p.multi_blk && e->side[region] &&
+                      handoff_fits(p.rpw, (int)depth, e->planes);
+    if (hand) {
+        a.side = e->side[region];
+        a.flags = e->flags[region];
+        a.err = e->d_err;
+        a.side_slot = (int64_t)2 * (depth - 1) * 64 * (e->planes / 2);
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = e->timing_every && (e->launch_count++ % e->timing_every) == 0;
     if (timed) {
@@ -573,12 +741,12 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         if (st != GOL_OK) return st;
         HIP_TRY(hipEventRecord(e0, s));
     }
-    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->var, e->planes, s));
+    HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->planes, hand, s));
     if (timed) {
         HIP_TRY(hipEventRecord(e1, s));
         e->ev_pending.push_back({e0, e1});
         double comp = 0;
-        for (const auto& s : p.segs) comp += (double)(s.out_hi - s.out_lo);
+        for (const auto& sg : p.segs) comp += (double)(sg.out_hi - sg.out_lo);
         e->pending_cells.push_back(p.own_rows * (double)e->W * depth);
         e->pending_cells_comp.push_back(comp * (double)e->W * depth);
     }
@@ -586,30 +754,98 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     return GOL_OK;
 }
 
-uint32_t pick_depth(uint32_t K, uint64_t remaining)
+// Order everything the side streams of a stripe engine have enqueued (band
+// launches, overlapped exchanges) before the next work on its compute stream, so
+// reads of the field on `stream` (store, digest) see the band rows.
+gol_status join_side_streams(gol_engine* e)
 {
-    for (int d : gol::kDepthList)
-        if ((uint32_t)d <= K && (uint64_t)d <= remaining) return (uint32_t)d;
-    return 1;
+    if (e->band_stream) {
+        HIP_TRY(hipEventRecord(e->ev_join, e->band_stream));
+        HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
+    }
+    if (e->comm_stream) {
+        HIP_TRY(hipEventRecord(e->ev_join, e->comm_stream));
+        HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
+    }
+    return GOL_OK;
+}
+
+// Before a load replaces the field: finish every stream of this engine and the
+// neighbours' exchange streams that may still be copying from its buffers.
+gol_status quiesce(gol_engine* e)
+{
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
+    if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (gol_engine* n : {e->up, e->down})
+        if (n && n->comm_stream) HIP_TRY(hipStreamSynchronize(n->comm_stream));
+    e->halo_fresh = false;
+    return GOL_OK;
+}
+
+// The kernel's hand-off wait gives up after a bounded time and flags it: report.
+gol_status check_err(gol_engine* e)
+{
+    if (!e->d_err) return GOL_OK;
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (!err) return GOL_OK;
+    HIP_TRY(hipMemset(e->d_err, 0, sizeof(int)));
+    for (int r = 0; r < 2; ++r)
+        if (e->flags[r]) {
+            const int64_t n = [&] {
+                int64_t m = 0;
+                for (const auto& p : e->plans) m = std::max(m, p.total_units);
+                return m;
+            }();
+            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)n * sizeof(uint32_t)));
+        }
+    return fail(GOL_EHIP, "row-block hand-off wait timed out in the stencil kernel; "
+                          "the field is not valid");
 }
 
 // Halo exchange (replaces exchangeGridData, Parallel_Life_MPI.cpp:104-145, whose
-// receives land in copies): Hx rows each way with the up/down neighbour.
+// receives land in copies): Hx rows each way with the up/down neighbour, over
+// RCCL or through the caller's host transport.
 gol_status exchange(gol_engine* e, hipStream_t st)
 {
     uint64_t* b = e->buf[e->cur];
     const size_t n = (size_t)e->Hx * e->stride;
     const size_t S = e->stride;
-    NCCL_TRY(ncclGroupStart());
-    if (e->rank > 0) {
-        NCCL_TRY(ncclSend(b + e->Hx * S, n, ncclUint64, e->rank - 1, e->comm, st));
-        NCCL_TRY(ncclRecv(b, n, ncclUint64, e->rank - 1, e->comm, st));
+    const bool has_up = e->rank > 0, has_dn = e->rank < e->nranks - 1;
+    if (e->xfer == XFER_RCCL) {
+        NCCL_TRY(ncclGroupStart());
+        if (has_up) {
+            NCCL_TRY(ncclSend(b + e->Hx * S, n, ncclUint64, e->rank - 1, e->comm, st));
+            NCCL_TRY(ncclRecv(b, n, ncclUint64, e->rank - 1, e->comm, st));
+        }
+        if (has_dn) {
+            NCCL_TRY(ncclSend(b + e->R * S, n, ncclUint64, e->rank + 1, e->comm, st));
+            NCCL_TRY(ncclRecv(b + (e->R + e->Hx) * S, n, ncclUint64, e->rank + 1, e->comm, st));
+        }
+        NCCL_TRY(ncclGroupEnd());
+        return GOL_OK;
     }
-    if (e->rank < e->nranks - 1) {
-        NCCL_TRY(ncclSend(b + e->R * S, n, ncclUint64, e->rank + 1, e->comm, st));
-        NCCL_TRY(ncclRecv(b + (e->R + e->Hx) * S, n, ncclUint64, e->rank + 1, e->comm, st));
-    }
-    NCCL_TRY(ncclGroupEnd());
+    if (e->xfer != XFER_HOST) return fail(GOL_ESTATE, "engine has no halo transport");
+    // host transport: stage the boundary rows, let the caller move them, copy back
+    uint64_t* send_up = e->host_xfer;
+    uint64_t* recv_up = send_up + n;
+    uint64_t* send_dn = recv_up + n;
+    uint64_t* recv_dn = send_dn + n;
+    if (has_up) HIP_TRY(hipMemcpyAsync(send_up, b + e->Hx * S, n * 8, hipMemcpyDeviceToHost, st));
+    if (has_dn) HIP_TRY(hipMemcpyAsync(send_dn, b + e->R * S, n * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const int rc = e->tp.exchange(e->tp.ctx, has_up ? send_up : nullptr, has_up ? recv_up : nullptr,
+                                  has_dn ? send_dn : nullptr, has_dn ? recv_dn : nullptr,
+                                  (uint64_t)(n * 8));
+    if (rc != 0)
+        return fail(GOL_EXFER, "halo transport callback returned " + std::to_string(rc));
+    if (has_up) HIP_TRY(hipMemcpyAsync(b, recv_up, n * 8, hipMemcpyHostToDevice, st));
+    if (has_dn)
+        HIP_TRY(hipMemcpyAsync(b + (e->R + e->Hx) * S, recv_dn, n * 8, hipMemcpyHostToDevice, st));
+    // the staging buffers are reused by the next exchange, on either stream
+    HIP_TRY(hipStreamSynchronize(st));
     return GOL_OK;
 }
 
@@ -675,7 +911,7 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
         *out = e;
         return GOL_OK;
     }
-    st = init_common(e, h, w, cfg);
+    st = init_common(e, h, w, cfg, nullptr);
     if (st != GOL_OK) {
         std::string msg = g_last_error;
         gol_destroy(e);
@@ -706,6 +942,61 @@ gol_status gol_comm_unique_id(uint8_t id[128])
     return GOL_OK;
 }
 
+gol_status gol_round_schedule(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
+                              uint64_t generations, int halo_fresh, gol_sched_op* ops,
+                              uint64_t cap, uint64_t* nops, uint32_t* tb_depth,
+                              uint32_t* halo_depth)
+{
+    if (!nops) return fail(GOL_EINVAL, "null nops");
+    gol_status st = check_cfg(cfg);
+    if (st != GOL_OK) return st;
+    if (h == 0 || w == 0) return fail(GOL_EINVAL, "h and w must be >= 1");
+    if (cfg->semantics != GOL_SEM_GLOBAL)
+        return fail(GOL_EINVAL, "rank engines implement GLOBAL semantics only");
+    RankGeom g;
+    st = rank_geometry(h, cfg, rank, nranks, &g);
+    if (st != GOL_OK) return st;
+    if (tb_depth) *tb_depth = g.K;
+    if (halo_depth) *halo_depth = (uint32_t)g.Hx;
+    std::vector<SchedOp> v;
+    if (nranks > 1) {
+        step_schedule(g.K, g.Hx, g.overlap, halo_fresh != 0 && g.overlap, generations, v);
+    } else {
+        for (uint64_t left = generations; left > 0;) {
+            const uint32_t d = pick_depth(g.K, left);
+            v.push_back({GOL_OP_LAUNCH, d, -1});
+            left -= d;
+        }
+    }
+    *nops = v.size();
+    if (ops) {
+        if (cap < v.size()) return fail(GOL_EINVAL, "schedule needs " + std::to_string(v.size()) + " ops");
+        uint32_t shrink = 0;
+        for (size_t i = 0; i < v.size(); ++i) {
+            gol_sched_op o{};
+            o.kind = v[i].kind;
+            o.depth = v[i].depth;
+            if (o.kind == GOL_OP_EXCHANGE || o.kind == GOL_OP_WAIT_EXCHANGE) shrink = 0;
+            if (o.kind == GOL_OP_LAUNCH || o.kind == GOL_OP_BAND) shrink += o.depth;
+            o.shrink = o.kind == GOL_OP_EXCHANGE_ASYNC ? 0 : shrink;
+            if (v[i].plan >= 0) {
+                const auto& segs = g.raw[(size_t)v[i].plan];
+                o.nseg = (uint32_t)std::min<size_t>(2, segs.size());
+                for (uint32_t k = 0; k < o.nseg; ++k) {
+                    o.out_lo[k] = segs[k].out_lo;
+                    o.out_hi[k] = segs[k].out_hi;
+                }
+            } else if (o.kind == GOL_OP_LAUNCH) {  // single stripe: the whole field
+                o.nseg = 1;
+                o.out_lo[0] = 0;
+                o.out_hi[0] = (int64_t)h;
+            }
+            ops[i] = o;
+        }
+    }
+    return GOL_OK;
+}
+
 }  // extern "C"
 
 namespace {
@@ -720,23 +1011,17 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     if (cfg->semantics != GOL_SEM_GLOBAL)
         return fail(GOL_EINVAL, "rank engines implement GLOBAL semantics only");
     if (h == 0 || w == 0) return fail(GOL_EINVAL, "h and w must be >= 1");
-    uint64_t row0, rows;
-    st = gol_rank_rows(h, nranks, rank, &row0, &rows);
+    RankGeom g;
+    st = rank_geometry(h, cfg, rank, nranks, &g);
     if (st != GOL_OK) return st;
-    const uint64_t minR = h / (uint64_t)nranks;
-    if (minR == 0) return fail(GOL_EINVAL, "fewer rows than ranks");
     gol_engine* e = new (std::nothrow) gol_engine();
     if (!e) return fail(GOL_ENOMEM, "host allocation");
     e->rank = rank;
     e->nranks = nranks;
-    e->row0 = row0;
-    e->R = rows;
-    const uint32_t K = auto_layout(rows, cfg).K;
-    // rounds of halo_depth generations between exchanges (default 8 launches)
-    uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 8 * (uint64_t)K;
-    if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
-    e->Hx = nranks > 1 ? Hx : 0;
-    st = init_common(e, h, w, cfg);
+    e->row0 = g.row0;
+    e->R = g.R;
+    e->Hx = g.Hx;
+    st = init_common(e, h, w, cfg, &g);
     if (st != GOL_OK) {
         std::string msg = g_last_error;
         gol_destroy(e);
@@ -766,6 +1051,29 @@ gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int ra
             gol_destroy(e);
             return fail(GOL_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
         }
+        e->xfer = XFER_RCCL;
+    }
+    *out = e;
+    return GOL_OK;
+}
+
+gol_status gol_create_rank_transport(uint64_t h, uint64_t w, const gol_config* cfg, int rank,
+                                     int nranks, const gol_transport* tp, gol_engine** out)
+{
+    if (!out || !tp || !tp->exchange) return fail(GOL_EINVAL, "null argument");
+    *out = nullptr;
+    gol_engine* e = nullptr;
+    gol_status st = make_rank_engine(h, w, cfg, rank, nranks, &e);
+    if (st != GOL_OK) return st;
+    if (nranks > 1) {
+        e->tp = *tp;
+        e->xfer = XFER_HOST;
+        const size_t bytes = 4 * (size_t)e->Hx * e->stride * sizeof(uint64_t);
+        hipError_t he = hipHostMalloc((void**)&e->host_xfer, bytes, hipHostMallocDefault);
+        if (he != hipSuccess) {
+            gol_destroy(e);
+            return fail(GOL_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(he));
+        }
     }
     *out = e;
     return GOL_OK;
@@ -785,6 +1093,7 @@ gol_status gol_create_group(uint64_t h, uint64_t w, const gol_config* cfg, int n
     for (int r = 0; r < nranks && st == GOL_OK; ++r) {
         gol_engine* e = engines[r];
         e->grouped = nranks > 1;
+        e->xfer = nranks > 1 ? XFER_GROUP : XFER_NONE;
         e->up = r > 0 ? engines[r - 1] : nullptr;
         e->down = r + 1 < nranks ? engines[r + 1] : nullptr;
         hipError_t he = hipSetDevice(e->device);
@@ -824,6 +1133,7 @@ void gol_destroy(gol_engine* e)
         delete e;
         return;
     }
+    (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
     if (e->band_stream) (void)hipStreamSynchronize(e->band_stream);
@@ -835,22 +1145,24 @@ void gol_destroy(gol_engine* e)
         if (n->band_stream) (void)hipStreamSynchronize(n->band_stream);
     }
     if (e->comm) (void)ncclCommDestroy(e->comm);
+    if (e->host_xfer) (void)hipHostFree(e->host_xfer);
     if (e->up) e->up->down = nullptr;
     if (e->down) e->down->up = nullptr;
     if (e->ev_ready) (void)hipEventDestroy(e->ev_ready);
     if (e->ev_copied) (void)hipEventDestroy(e->ev_copied);
-    if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
-    if (e->band_stream) (void)hipStreamSynchronize(e->band_stream);
-    if (e->ev_band) (void)hipEventDestroy(e->ev_band);
-    if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+    for (hipEvent_t ev : {e->ev_band, e->ev_in, e->ev_xdone, e->ev_join})
+        if (ev) (void)hipEventDestroy(ev);
     if (e->band_stream) (void)hipStreamDestroy(e->band_stream);
-    if (e->ev_xdone) (void)hipEventDestroy(e->ev_xdone);
     if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
     for (auto& p : e->plans)
         if (p.dev) (void)hipFree(p.dev);
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < 2; ++b) {
         if (e->alloc[b]) (void)hipFree(e->alloc[b]);
-    for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.first);
+        if (e->side[b]) (void)hipFree(e->side[b]);
+        if (e->flags[b]) (void)hipFree(e->flags[b]);
+    }
+    if (e->d_err) (void)hipFree(e->d_err);
+    for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.exec);
     if (e->d_acc) (void)hipFree(e->d_acc);
     if (e->d_flag) (void)hipFree(e->d_flag);
     for (auto& p : e->ev_pending) {
@@ -883,11 +1195,7 @@ static uint64_t load_rows_needed(const gol_engine* e)
 // engine's lane groups (bitlayout.h).
 static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs)
 {
-    HIP_TRY(hipSetDevice(e->device));
-    if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
-    if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    e->halo_fresh = false;
+    GOL_TRY(quiesce(e));
     // clear everything (halos, unused rows) then copy each region, masking pad bits
     const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
     HIP_TRY(hipMemsetAsync(e->alloc[e->cur], 0, words_all * 8, e->stream));
@@ -918,6 +1226,7 @@ static gol_status upload(gol_engine* e, const uint64_t* words, uint64_t rs)
 static gol_status download(gol_engine* e, uint64_t* words, uint64_t rs)
 {
     HIP_TRY(hipSetDevice(e->device));
+    GOL_TRY(join_side_streams(e));
     std::vector<uint64_t> tmp;
     for (const auto& r : e->user_regions) {
         tmp.resize((size_t)r.rows * e->stride);
@@ -937,7 +1246,7 @@ static gol_status download(gol_engine* e, uint64_t* words, uint64_t rs)
             }
         }
     }
-    return GOL_OK;
+    return check_err(e);
 }
 
 // composite engines: part r holds field rows [row0_r, row0_r + rows_r)
@@ -985,11 +1294,7 @@ gol_status gol_load_ascii(gol_engine* e, const char* buf, size_t len)
                                     std::to_string(rows * (e->W + 1)) + ", got " +
                                     std::to_string(len));
     // raw bytes to the device, packed there by the ASCII codec kernel
-    HIP_TRY(hipSetDevice(e->device));
-    if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
-    if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    e->halo_fresh = false;
+    GOL_TRY(quiesce(e));
     DeviceBytes bytes;
     HIP_TRY(hipMalloc(&bytes.p, len));
     HIP_TRY(hipMemcpyAsync(bytes.p, buf, len, hipMemcpyHostToDevice, e->stream));
@@ -1046,6 +1351,7 @@ gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
         return fail(GOL_EINVAL, "ASCII length must be rows*(w+1) = " +
                                     std::to_string(rows * (e->W + 1)));
     HIP_TRY(hipSetDevice(e->device));
+    GOL_TRY(join_side_streams(e));
     DeviceBytes bytes;
     HIP_TRY(hipMalloc(&bytes.p, len));
     for (const auto& r : e->user_regions) {
@@ -1057,7 +1363,7 @@ gol_status gol_store_ascii(gol_engine* e, char* buf, size_t len)
     }
     HIP_TRY(hipMemcpyAsync(buf, bytes.p, len, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    return GOL_OK;
+    return check_err(e);
 }
 
 gol_status gol_init_random(gol_engine* e, uint64_t seed)
@@ -1070,11 +1376,7 @@ gol_status gol_init_random(gol_engine* e, uint64_t seed)
         }
         return GOL_OK;
     }
-    HIP_TRY(hipSetDevice(e->device));
-    if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
-    if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    e->halo_fresh = false;
+    GOL_TRY(quiesce(e));
     const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
     HIP_TRY(hipMemsetAsync(e->alloc[e->cur], 0, words_all * 8, e->stream));
     for (const auto& r : e->load_regions)
@@ -1088,43 +1390,6 @@ gol_status gol_init_random(gol_engine* e, uint64_t seed)
 }  // extern "C"
 
 namespace {
-
-// The launches of one round of `round` generations after a halo exchange: each
-// launch of depth d shrinks the valid region by d rows per side (plan c-1 for a
-// cumulative shrink of c).
-// The launches of one round of `round` generations after a halo exchange: each
-// launch of depth d shrinks the valid region by d rows per side (plan c-1 for a
-// cumulative shrink of c).  With overlap, the last launch of a full round runs
-// as band + interior and `xchg` (the transport) is called between them; it must
-// start the next round's exchange on e->comm_stream after e->ev_band.
-template <class Xchg>
-gol_status run_round(gol_engine* e, uint64_t round, Xchg&& xchg)
-{
-    uint64_t done = 0;
-    while (done < round) {
-        const uint32_t d = pick_depth(e->K, round - done);
-        done += d;
-        gol_status st;
-        if (e->overlap && done == e->Hx) {
-            // band rows on the band stream, concurrent with the interior launch
-            HIP_TRY(hipEventRecord(e->ev_in, e->stream));
-            HIP_TRY(hipStreamWaitEvent(e->band_stream, e->ev_in, 0));
-            st = launch(e, (int)e->Hx, d, false, e->band_stream);
-            if (st != GOL_OK) return st;
-            HIP_TRY(hipEventRecord(e->ev_band, e->band_stream));
-            st = launch(e, (int)e->Hx + 1, d, false);  // interior, overlaps the exchange
-            if (st != GOL_OK) return st;
-            e->cur ^= 1;
-            st = xchg();
-            if (st != GOL_OK) return st;
-            e->halo_fresh = true;
-        } else {
-            st = launch(e, (int)(done - 1), d);
-        }
-        if (st != GOL_OK) return st;
-    }
-    return GOL_OK;
-}
 
 // Loopback exchange of a group member on stream `st`: pull the neighbours'
 // boundary rows into this engine's halo rows (same layout as the RCCL exchange).
@@ -1167,39 +1432,51 @@ gol_status wait_fresh_halos(gol_engine* e)
     return GOL_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-gol_status gol_step(gol_engine* e, uint64_t generations)
+// Run one launch op of a stripe engine's schedule.  `xchg` starts the
+// overlapped exchange after a band launch (on comm_stream after ev_band).
+template <class Xchg>
+gol_status run_launch_op(gol_engine* e, const SchedOp& op, Xchg&& xchg)
 {
-    if (!e) return fail(GOL_EINVAL, "null engine");
-    if (!e->parts.empty()) return gol_group_step(e->parts.data(), (int)e->parts.size(), generations);
-    if (e->grouped) return fail(GOL_ESTATE, "group members advance with gol_group_step");
-    HIP_TRY(hipSetDevice(e->device));
-    uint64_t left = generations;
-    if (e->nranks > 1) {
-        auto xchg = [e]() -> gol_status {  // overlapped: on comm after the band launch
-            HIP_TRY(hipStreamWaitEvent(e->comm_stream, e->ev_band, 0));
-            gol_status st = exchange(e, e->comm_stream);
-            if (st != GOL_OK) return st;
-            HIP_TRY(hipEventRecord(e->ev_xdone, e->comm_stream));
-            return GOL_OK;
-        };
-        while (left > 0) {
-            const uint64_t round = std::min<uint64_t>(left, e->Hx);
-            gol_status st = e->halo_fresh ? wait_fresh_halos(e) : exchange(e, e->stream);
-            if (st == GOL_OK) st = run_round(e, round, xchg);
-            if (st != GOL_OK) return st;
-            left -= round;
-        }
+    switch (op.kind) {
+    case GOL_OP_LAUNCH: return launch(e, op.plan, op.depth);
+    case GOL_OP_BAND:
+        // band rows on the band stream, concurrent with the interior launch
+        HIP_TRY(hipEventRecord(e->ev_in, e->stream));
+        HIP_TRY(hipStreamWaitEvent(e->band_stream, e->ev_in, 0));
+        GOL_TRY(launch(e, op.plan, op.depth, false, e->band_stream));
+        HIP_TRY(hipEventRecord(e->ev_band, e->band_stream));
         return GOL_OK;
+    case GOL_OP_INTERIOR:
+        GOL_TRY(launch(e, op.plan, op.depth, false));  // interior, overlaps the exchange
+        e->cur ^= 1;
+        return GOL_OK;
+    case GOL_OP_EXCHANGE_ASYNC:
+        GOL_TRY(xchg());
+        e->halo_fresh = true;
+        return GOL_OK;
+    default: return fail(GOL_ESTATE, "bad schedule op");
     }
+}
+
+// Single-stream engines: the launch sequence of gol_step(gens) as a captured
+// hipGraph, replayed from the second call on (LRU cache keyed by gens and the
+// starting buffer).
+gol_status step_single(gol_engine* e, uint64_t generations)
+{
+    uint64_t left = generations;
     const bool graphable = e->timing_every == 0 && generations >= 4 * (uint64_t)e->K;
     if (graphable) {
         const auto key = std::make_pair(generations, e->cur);
         auto it = e->graphs.find(key);
         if (it == e->graphs.end()) {
+            if (e->graphs.size() >= kGraphCache) {
+                auto lru = e->graphs.begin();
+                for (auto j = e->graphs.begin(); j != e->graphs.end(); ++j)
+                    if (j->second.used < lru->second.used) lru = j;
+                HIP_TRY(hipStreamSynchronize(e->stream));
+                (void)hipGraphExecDestroy(lru->second.exec);
+                e->graphs.erase(lru);
+            }
             hipGraph_t g = nullptr;
             HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
             const int cur0 = e->cur;
@@ -1226,18 +1503,49 @@ gol_status gol_step(gol_engine* e, uint64_t generations)
                 e->cur = cur0;
                 return fail(GOL_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
             }
-            it = e->graphs.emplace(key, std::make_pair(x, e->cur)).first;
+            it = e->graphs.emplace(key, gol_engine::GraphEntry{x, e->cur, 0}).first;
             e->cur = cur0;
         }
-        HIP_TRY(hipGraphLaunch(it->second.first, e->stream));
-        e->cur = it->second.second;
+        it->second.used = ++e->graph_clock;
+        HIP_TRY(hipGraphLaunch(it->second.exec, e->stream));
+        e->cur = it->second.cur_after;
         return GOL_OK;
     }
     while (left > 0) {
         const uint32_t d = pick_depth(e->K, left);
-        gol_status st = launch(e, 0, d);
-        if (st != GOL_OK) return st;
+        GOL_TRY(launch(e, 0, d));
         left -= d;
+    }
+    return GOL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+gol_status gol_step(gol_engine* e, uint64_t generations)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) return gol_group_step(e->parts.data(), (int)e->parts.size(), generations);
+    if (e->grouped) return fail(GOL_ESTATE, "group members advance with gol_group_step");
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->nranks <= 1) return step_single(e, generations);
+    auto xchg = [e]() -> gol_status {  // overlapped: on comm after the band launch
+        HIP_TRY(hipStreamWaitEvent(e->comm_stream, e->ev_band, 0));
+        GOL_TRY(exchange(e, e->comm_stream));
+        HIP_TRY(hipEventRecord(e->ev_xdone, e->comm_stream));
+        return GOL_OK;
+    };
+    std::vector<SchedOp> ops;
+    step_schedule(e->K, e->Hx, e->overlap, e->halo_fresh, generations, ops);
+    for (const SchedOp& op : ops) {
+        if (op.kind == GOL_OP_EXCHANGE) {
+            GOL_TRY(exchange(e, e->stream));
+        } else if (op.kind == GOL_OP_WAIT_EXCHANGE) {
+            GOL_TRY(wait_fresh_halos(e));
+        } else {
+            GOL_TRY(run_launch_op(e, op, xchg));
+        }
     }
     return GOL_OK;
 }
@@ -1251,11 +1559,26 @@ gol_status gol_group_step(gol_engine** engines, int nranks, uint64_t generations
             return fail(GOL_EINVAL, "engines must be the members of one group, in rank order");
     }
     if (nranks == 1) return gol_step(engines[0], generations);
-    const uint64_t Hx = engines[0]->Hx;
-    uint64_t left = generations;
-    while (left > 0) {
-        const uint64_t round = std::min<uint64_t>(left, Hx);
-        if (!engines[0]->halo_fresh) {
+    // every member runs the same schedule (same K, Hx and overlap decision); a
+    // member whose halos are not fresh (a reload) makes the round exchange block
+    bool fresh = true;
+    for (int r = 0; r < nranks; ++r) fresh &= engines[r]->halo_fresh;
+    if (!fresh)
+        for (int r = 0; r < nranks; ++r) {
+            gol_engine* e = engines[r];
+            if (e->halo_fresh) {  // its overlapped pulls must land before the new ones
+                HIP_TRY(hipSetDevice(e->device));
+                GOL_TRY(wait_fresh_halos(e));
+            }
+            e->halo_fresh = false;
+        }
+    std::vector<SchedOp> ops;
+    step_schedule(engines[0]->K, engines[0]->Hx, engines[0]->overlap, fresh, generations, ops);
+    size_t i = 0;
+    while (i < ops.size()) {
+        // one round: its exchange op, then the launches up to the next exchange
+        const SchedOp& x = ops[i++];
+        if (x.kind == GOL_OP_EXCHANGE) {
             // blocking exchange on the compute streams (first round after a load)
             for (int r = 0; r < nranks; ++r) {  // every member's state is final
                 gol_engine* e = engines[r];
@@ -1265,8 +1588,7 @@ gol_status gol_group_step(gol_engine** engines, int nranks, uint64_t generations
             for (int r = 0; r < nranks; ++r) {
                 gol_engine* e = engines[r];
                 HIP_TRY(hipSetDevice(e->device));
-                gol_status st = pull_halos(e, e->stream, &gol_engine::ev_ready);
-                if (st != GOL_OK) return st;
+                GOL_TRY(pull_halos(e, e->stream, &gol_engine::ev_ready));
                 HIP_TRY(hipEventRecord(e->ev_copied, e->stream));
             }
             for (int r = 0; r < nranks; ++r) {  // neighbours done reading my rows
@@ -1278,33 +1600,35 @@ gol_status gol_group_step(gol_engine** engines, int nranks, uint64_t generations
         } else {
             for (int r = 0; r < nranks; ++r) {
                 HIP_TRY(hipSetDevice(engines[r]->device));
-                gol_status st = wait_fresh_halos(engines[r]);
-                if (st != GOL_OK) return st;
+                GOL_TRY(wait_fresh_halos(engines[r]));
             }
         }
+        size_t j = i;
+        while (j < ops.size() && ops[j].kind != GOL_OP_EXCHANGE &&
+               ops[j].kind != GOL_OP_WAIT_EXCHANGE)
+            ++j;
         // launches; the overlapped pulls are issued once every member has
-        // recorded its band event (the lambda only marks the member ready)
+        // recorded its band event (the callback only marks the round)
         bool pulls_due = false;
         for (int r = 0; r < nranks; ++r) {
             gol_engine* e = engines[r];
             HIP_TRY(hipSetDevice(e->device));
-            gol_status st = run_round(e, round, [&pulls_due]() -> gol_status {
-                pulls_due = true;
-                return GOL_OK;
-            });
-            if (st != GOL_OK) return st;
+            for (size_t k = i; k < j; ++k)
+                GOL_TRY(run_launch_op(e, ops[k], [&pulls_due]() -> gol_status {
+                    pulls_due = true;
+                    return GOL_OK;
+                }));
         }
         if (pulls_due) {
             for (int r = 0; r < nranks; ++r) {
                 gol_engine* e = engines[r];
                 HIP_TRY(hipSetDevice(e->device));
                 HIP_TRY(hipStreamWaitEvent(e->comm_stream, e->ev_band, 0));
-                gol_status st = pull_halos(e, e->comm_stream, &gol_engine::ev_band);
-                if (st != GOL_OK) return st;
+                GOL_TRY(pull_halos(e, e->comm_stream, &gol_engine::ev_band));
                 HIP_TRY(hipEventRecord(e->ev_xdone, e->comm_stream));
             }
         }
-        left -= round;
+        i = j;
     }
     return GOL_OK;
 }
@@ -1319,10 +1643,11 @@ gol_status gol_sync(gol_engine* e)
         }
         return GOL_OK;
     }
+    HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     if (e->band_stream) HIP_TRY(hipStreamSynchronize(e->band_stream));
     if (e->comm_stream) HIP_TRY(hipStreamSynchronize(e->comm_stream));
-    return GOL_OK;
+    return check_err(e);
 }
 
 gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
@@ -1342,6 +1667,7 @@ gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
         return GOL_OK;
     }
     HIP_TRY(hipSetDevice(e->device));
+    GOL_TRY(join_side_streams(e));
     HIP_TRY(hipMemsetAsync(e->d_acc, 0, 2 * sizeof(unsigned long long), e->stream));
     for (const auto& r : e->user_regions)
         HIP_TRY(gol::launch_digest(e->buf[e->cur], (int64_t)e->stride, (int64_t)e->wq,
@@ -1352,7 +1678,7 @@ gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
     HIP_TRY(hipStreamSynchronize(e->stream));
     *live = acc[0];
     *hash = acc[1];
-    return GOL_OK;
+    return check_err(e);
 }
 
 gol_status gol_set_timing(gol_engine* e, int every)
@@ -1415,7 +1741,8 @@ gol_status gol_reset_timing(gol_engine* e)
 gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uint64_t* rows,
                     uint32_t* tb_depth, uint32_t* halo_depth, uint32_t* rows_per_wave)
 {
-    if (e && !e->parts.empty()) {
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) {
         gol_status st = gol_info(e->parts[0], nullptr, nullptr, nullptr, nullptr, tb_depth,
                                  halo_depth, rows_per_wave);
         if (st != GOL_OK) return st;
@@ -1425,8 +1752,7 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uin
         if (rows) *rows = e->H;
         return GOL_OK;
     }
-    if (e && rows_per_wave) *rows_per_wave = e->plans.empty() ? 0 : (uint32_t)e->plans.back().rpw;
-    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (rows_per_wave) *rows_per_wave = e->plans.empty() ? 0 : (uint32_t)e->plans.back().rpw;
     if (h) *h = e->H;
     if (w) *w = e->W;
     if (row0) *row0 = e->row0;
@@ -1448,6 +1774,18 @@ gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_pe
     const auto& p = e->nranks > 1 ? e->plans[e->Hx - 1] : e->plans[0];
     if (strip_lanes) *strip_lanes = (uint32_t)(64 >> p.lane_shift);
     if (rows_per_wave) *rows_per_wave = (uint32_t)p.rpw;
+    return GOL_OK;
+}
+
+gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff)
+{
+    if (!e || !handoff) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) return gol_plan_handoff(e->parts[0], handoff);
+    if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
+    const auto& p = e->nranks > 1 ? e->plans[e->Hx - 1] : e->plans[0];
+    *handoff = (p.hand && p.multi_blk && e->side[0] && handoff_fits(p.rpw, (int)e->K, e->planes))
+                   ? 1u
+                   : 0u;
     return GOL_OK;
 }
 

@@ -1,8 +1,13 @@
 // Internal interface between the host engine (engine.cpp) and the HIP kernels
-// (life_kernels.hip).  Not part of the public C ABI (include/gol.h).
+// (life_stencil.h, life_tb_d*.hip, life_aux.hip).  Not part of the public C ABI
+// (include/gol.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#ifndef GOL_DEV_KERNELS
+#define GOL_DEV_KERNELS 0
+#endif
 
 namespace gol {
 
@@ -32,9 +37,10 @@ struct SegDesc {
 // Strips: a strip is L consecutive lanes (L = 64 >> lane_shift: 64, 32 or 16),
 // each holding one lane group of a row (NP 32-bit planes = NP/2 words,
 // bitlayout.h); its first and last lane are the horizontal halo (exact for up to
-// 63 fused generations), so a strip outputs L - 2 groups.  A wavefront runs 64 / L strips side by side over the same rows:
-// narrow strips trade 2 halo lanes per strip for more wavefronts per row block,
-// which lets short stripes use longer row blocks (less vertical halo recompute).
+// 63 fused generations), so a strip outputs L - 2 groups.  A wavefront runs 64 / L
+// strips side by side over the same rows: narrow strips trade 2 halo lanes per
+// strip for more wavefronts per row block, which lets short stripes use longer row
+// blocks (less vertical halo recompute).
 constexpr int kStripOut = 62;  // output lane groups of a full 64-lane strip
 constexpr int kWavesPerBlock = 4;
 // Zeroed guard rows allocated before/after every state buffer so that the
@@ -49,30 +55,60 @@ struct StepArgs {
     int32_t nseg;
     int32_t strips;       // strip groups per row: ceil(ceil(wq / (L-2)) / (64/L))
     int32_t lane_shift;   // L = 64 >> lane_shift lanes per strip (0, 1 or 2)
+    int32_t pad0;
     int64_t stride;       // words per buffer row
     int64_t ng;           // lane groups per field row = ceil(ceil(w / 64) / (NP/2))
     uint64_t lastmask[2]; // stored-form valid bits of the last group's words
     int64_t rows_per_wave;
     int64_t total_units;  // wavefronts in the launch
     uint32_t birth, survive;
+    // Row-block hand-off (kernels instantiated with HAND = true; see
+    // life_stencil.h): each wavefront's slot of side rows, its ready flag, and a
+    // flag the kernel sets when a wait for a neighbour's rows timed out.
+    uint64_t* side;       // total_units slots of side_slot words
+    uint32_t* flags;      // total_units words, all 0 between launches
+    int* err;
+    int64_t side_slot;    // words per slot: 2 (K-1) rows x 64 lanes x NP/2 words
 };
 
-// Fused depths with an instantiated kernel, largest first.
+// Fused depths with an instantiated kernel, largest first.  The shipped library
+// builds the depths auto_layout and the remainder launches use; the dev build
+// (make dev, GOL_DEV_KERNELS) adds 20/24/32 and the 4-plane lane groups.
+#if GOL_DEV_KERNELS
 constexpr int kDepthList[] = {32, 24, 20, 16, 12, 8, 7, 6, 4, 2, 1};
+#else
+constexpr int kDepthList[] = {16, 12, 8, 7, 6, 4, 2, 1};
+#endif
+constexpr bool kDevKernels = GOL_DEV_KERNELS != 0;
+
+// Row blocks hand their first rows of every fused generation to the block above
+// (life_stencil.h) from this depth on.
+constexpr int kHandoffMinDepth = 4;
+
+// Steps per block of the stencil kernel's register prefetch ring (host copy of
+// life_stencil.h kPfOf): 8 for 2-plane kernels of depth >= 16, 4 elsewhere.
+constexpr int prefetch_of(int K, int planes) { return (planes == 2 && K >= 16) ? 8 : 4; }
+// Unrolled warm-up steps (a multiple of the prefetch block covering 2K steps).
+constexpr int warm_steps_of(int K, int planes)
+{
+    return (2 * K + prefetch_of(K, planes) - 1) / prefetch_of(K, planes) * prefetch_of(K, planes);
+}
 
 // Launch `depth` fused generations (depth in kDepthList) on lane groups of
-// `planes` (2 or 4) planes.  `var` = kernel variant: 0 total-sum stage state (5
-// planes per fused generation), anti-diagonal schedule (default); 1
-// neighbour-sum state (7 planes, +4 VALU ops per plane-generation),
-// anti-diagonal; 2 as 0 with the step-major schedule (kept for A/B
-// measurements).  life_has_kernel tells which combinations exist.
-hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int var, int planes,
+// `planes` (2, or 4 in the dev build).  hand: the row-block hand-off kernel
+// (a.side/flags/err set); else every row block recomputes its vertical halo.
+hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int planes, bool hand,
                        hipStream_t s);
-bool life_has_kernel(int depth, int var, int planes);
+bool life_has_kernel(int depth, int planes);
 
-// Resident 256-thread blocks per CU of the stencil kernel for (depth, rule,
-// variant, planes) -- each block is one wavefront per SIMD (occupancy query).
-int life_blocks_per_cu(int depth, RuleKind rule, int var, int planes);
+// Resident 256-thread blocks per CU of the stencil kernel (occupancy query).
+int life_blocks_per_cu(int depth, RuleKind rule, int planes, bool hand);
+
+// Per-depth entry points (explicitly instantiated in life_tb_d<K>.hip).
+template <int K>
+hipError_t launch_depth(const StepArgs& a, RuleKind rule, int planes, bool hand, hipStream_t s);
+template <int K>
+int occupancy_depth(RuleKind rule, int planes, bool hand);
 
 // Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field
 // rows [glob_row0, glob_row0+nrows).

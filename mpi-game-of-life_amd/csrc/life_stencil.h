@@ -1,0 +1,606 @@
+// life_stencil.h -- the gfx950 stencil kernel of the Game of Life engine.
+//
+// Hot path: the per-generation update of Parallel_Life_MPI.cpp (countNeighbours
+// :16-35 + updateGrid :37-54), restated on a bit-packed field (64 cells per
+// uint64) and fused over K generations per launch (temporal blocking).  Included
+// by one translation unit per depth (life_tb_d<K>.hip), which instantiates
+// life_tb_kernel<K, RULE, NP, HAND> for the three rule kinds.
+//
+// Kernel shape (one wavefront = one work unit, no LDS, no block barriers):
+//   * A wavefront owns a strip of 64 consecutive lane groups of a row (lane l
+//     holds group strip*62 - 1 + l); lanes 0 and 63 are the horizontal halo, so
+//     each strip outputs 62 groups.  A lane group is NP = 2 (or, dev build, 4)
+//     planes of 32 cells (bitlayout.h: column NP*j + k of the group at bit j of
+//     plane k), so the horizontal neighbours of every plane but the first and
+//     last are other planes at the same bit; those two take one v_alignbit each,
+//     with the carry bit from the adjacent lane by a DPP wave shift.  After g
+//     fused generations the contamination from the unknown groups beyond the
+//     halo lanes has moved g columns into lanes 0/63, so K <= 63 keeps lanes
+//     1..62 exact.
+//   * The wavefront streams down the rows of its row block.  Generation g
+//     (stage g-1, g = 1..K) keeps a 3-row window in registers: for each incoming
+//     row it forms the horizontal 3-cell sum H3 (bit-sliced sum + carry) once and
+//     emits the previous row from the 9-cell total H3(r-2) + H3(r-1) + H3(r).
+//     Stage s consumes the row stage s-1 emitted in the same step.  Each input row
+//     is read once from HBM and each output row written once per K generations.
+//   * Field rows outside [0, field_h) are dead (Parallel_Life_MPI.cpp:21-22) and
+//     columns >= w are dead (:26-27): masked on load and -- for rules that can
+//     give birth -- re-masked after every generation.
+//
+// Row blocks (R output rows each, rb..re).  Step t ingests input row rb - K + t;
+// stage s emits row rb - K + t - (s+1) at step t, so generation g is computed
+// for rows [rb - K + g, ...) and the K rows of input above the block are its
+// vertical halo.  Two ways to close the block at the bottom:
+//   * classic (HAND = false, and the last block of every segment): keep
+//     streaming K rows past re; stage s computes R + 2(K - s - 1) rows, i.e. every
+//     block recomputes K(K-1) stage-steps of its neighbour's rows.
+//   * hand-off (HAND = true): the block's generation-g rows end at re - K + g and
+//     the two generation-(g-1) rows stage g-1 needs beyond that come from the
+//     block below, which computed them first thing (its first two rows of every
+//     generation).  Each block writes those 2(K-1) "side rows" to its slot,
+//     signals a flag, and the block above reads them at the end of its stream:
+//     stage s computes exactly R + 2 rows.  Blocks are numbered bottom-up, so a
+//     block's producer always has the smaller wavefront index (dispatched no
+//     later); waits are bounded and a timeout sets *err instead of hanging.
+//     Hand-off memory protocol (MI355X_MICROARCH.md, inter-workgroup
+//     visibility, first table row): side rows stored write-through (sc1), the
+//     producer's s_waitcnt vmcnt(0), an sc1 flag store by one lane; the consumer
+//     polls with sc1 loads and reads the rows with sc1 loads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "bitlayout.h"
+#include "life_internal.h"
+#include "loop_place.h"
+
+namespace gol {
+
+namespace {
+
+__device__ __forceinline__ uint32_t lane_from_left(uint32_t v)
+{
+    // DPP wave_shr:1 -- lane l receives lane l-1's value; lane 0 receives 0.
+    return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t lane_from_right(uint32_t v)
+{
+    // DPP wave_shl:1 -- lane l receives lane l+1's value; lane 63 receives 0.
+    return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xf, 0xf, true);
+}
+
+// The NP 32-bit cell planes of one lane group (bitlayout.h): NP/2 words, 32*NP
+// columns; plane k bit j = column NP*j + k of the group.
+template <int NP>
+struct Pl {
+    uint32_t v[NP];
+};
+
+// The group's words as stored in HBM: one 8- (NP = 2) or 16-byte (NP = 4) access.
+template <int NP>
+struct alignas(4 * NP) Grp {
+    uint64_t w[NP / 2];
+};
+
+template <int NP>
+__device__ __forceinline__ Pl<NP> planes_of(const Grp<NP>& g)
+{
+    Pl<NP> p;
+#pragma unroll
+    for (int i = 0; i < NP / 2; ++i) {
+        p.v[2 * i] = (uint32_t)g.w[i];
+        p.v[2 * i + 1] = (uint32_t)(g.w[i] >> 32);
+    }
+    return p;
+}
+template <int NP>
+__device__ __forceinline__ Grp<NP> words_of(const Pl<NP>& p)
+{
+    Grp<NP> g;
+#pragma unroll
+    for (int i = 0; i < NP / 2; ++i) g.w[i] = ((uint64_t)p.v[2 * i + 1] << 32) | p.v[2 * i];
+    return g;
+}
+
+// Loads and stores of the row stream.  Every load of the stream is an agent-scope
+// relaxed atomic (global_load ... sc1: served by L2, not the CU's L1), so the same
+// code reads the input field and, at the end of a hand-off block, the side rows
+// another wavefront stored write-through.
+template <int NP>
+__device__ __forceinline__ Grp<NP> load_grp(const uint64_t* p)
+{
+    Grp<NP> g;
+#pragma unroll
+    for (int i = 0; i < NP / 2; ++i)
+        g.w[i] = __hip_atomic_load(const_cast<uint64_t*>(p + i), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    return g;
+}
+template <int NP>
+__device__ __forceinline__ void store_side(uint64_t* p, const Pl<NP>& x)
+{
+    const Grp<NP> g = words_of(x);
+#pragma unroll
+    for (int i = 0; i < NP / 2; ++i)
+        __hip_atomic_store(p + i, g.w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// v_bitop3_b32: any 3-input bitwise function in one VALU op.  The immediate is
+// the function's truth table evaluated on S0 = 0xF0, S1 = 0xCC, S2 = 0xAA.
+template <uint32_t LUT>
+__device__ __forceinline__ uint32_t lop3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, LUT);
+}
+constexpr uint32_t kXor3 = 0x96;      // a ^ b ^ c
+constexpr uint32_t kMaj = 0xE8;       // majority(a, b, c): carry of a + b + c
+constexpr uint32_t kTwoThree = 0x14;  // (a ^ b) & ~c
+constexpr uint32_t kAnd3 = 0x80;      // a & b & c
+constexpr uint32_t kFour = 0x42;      // ~(a ^ b) & (a ^ c)
+constexpr uint32_t kAndNot = 0x40;    // a & b & ~c
+constexpr uint32_t kOrAnd2 = 0xEA;    // (a & b) | c
+
+// Horizontal neighbours of a lane group x (bitlayout.h).  Plane k's left
+// neighbours are plane k-1 and its right neighbours plane k+1, at the same bit,
+// except at the two ends: plane 0's left neighbours are plane NP-1 shifted up one
+// bit (its bit 0 from the last plane of the group to the left, in lane l-1), and
+// plane NP-1's right neighbours are plane 0 shifted down one bit (bit 31 from
+// lane l+1).  One DPP wave shift and one v_alignbit each, per group.
+struct Ends {
+    uint32_t l0, rn;
+};
+template <int NP>
+__device__ __forceinline__ Ends ends(const Pl<NP>& x)
+{
+    const uint32_t hp = lane_from_left(x.v[NP - 1]);  // bit 31: the column left of the group
+    const uint32_t ln = lane_from_right(x.v[0]);      // bit 0: the column right of the group
+    Ends e;
+    e.l0 = __builtin_amdgcn_alignbit(x.v[NP - 1], hp, 31);  // (last << 1) | (hp >> 31)
+    e.rn = __builtin_amdgcn_alignbit(ln, x.v[0], 1);        // (first >> 1) | (ln << 31)
+    return e;
+}
+template <int NP>
+__device__ __forceinline__ uint32_t left_of(const Pl<NP>& x, const Ends& e, int k)
+{
+    return k == 0 ? e.l0 : x.v[k - 1];
+}
+template <int NP>
+__device__ __forceinline__ uint32_t right_of(const Pl<NP>& x, const Ends& e, int k)
+{
+    return k == NP - 1 ? e.rn : x.v[k + 1];
+}
+
+// Stage state (5 planes per fused generation): H3 of rows r-2 and r-1 and the
+// cells of row r-1.  The emitted cell sees T = H3(r-2) + H3(r-1) + H3(r), the
+// 9-cell sum including itself.  For an alive cell T = n + 1, for a dead one T = n
+// (generic masks: survive bit T-1 / birth bit T); the two fixed rules read it off
+// directly:
+//   REF (B/S2):      next = alive && T == 3   (Parallel_Life_MPI.cpp:47-50)
+//   CONWAY (B3/S23): next = T == 3 || (alive && T == 4)
+template <int NP>
+struct StageT {
+    Pl<NP> ps, pc;
+    Pl<NP> cs, cc;
+    Pl<NP> al;
+};
+
+template <int RULE>
+__device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint32_t bs,
+                                                 uint32_t bc, uint32_t es, uint32_t ec,
+                                                 uint32_t alive, uint32_t birth,
+                                                 uint32_t survive)
+{
+    // T = A + B + E, each a 2-bit H3 sum: T = s0 + 2*(p + k0) + 4*mj (0..9)
+    const uint32_t s0 = lop3<kXor3>(as, bs, es);
+    const uint32_t k0 = lop3<kMaj>(as, bs, es);
+    const uint32_t p = lop3<kXor3>(ac, bc, ec);
+    const uint32_t mj = lop3<kMaj>(ac, bc, ec);
+    // T == 3  <=>  s0 && p + k0 == 1 && !mj
+    const uint32_t three = lop3<kTwoThree>(p, k0, mj);
+    if constexpr (RULE == RULE_REF) {
+        // Parallel_Life_MPI.cpp:47-50: alive && n == 2  <=>  alive && T == 3
+        return lop3<kAnd3>(alive, s0, three);
+    } else if constexpr (RULE == RULE_CONWAY) {
+        // T == 4  <=>  !s0 && (p + k0 == 2 && !mj  ||  p + k0 == 0 && mj)
+        const uint32_t four = lop3<kFour>(p, k0, mj);
+        const uint32_t stay = lop3<kAndNot>(alive, four, s0);  // alive & four & !s0
+        return lop3<kOrAnd2>(s0, three, stay);                 // (s0 & three) | stay
+    } else {
+        // T = s0 + 2*x + 4*t2 + 8*t3; alive cells have n = T - 1, dead ones n = T
+        const uint32_t x = p ^ k0, y = p & k0;
+        const uint32_t t2 = y ^ mj, t3 = y & mj;
+        uint32_t r = 0;
+#pragma unroll
+        for (int v = 0; v <= 9; ++v) {
+            const uint32_t ssel = v >= 1 ? (survive >> (v - 1)) & 1u : 0u;
+            const uint32_t bsel = v <= 8 ? (birth >> v) & 1u : 0u;
+            if (bsel | ssel) {
+                const uint32_t eq = ((v & 1) ? s0 : ~s0) & ((v & 2) ? x : ~x) &
+                                    ((v & 4) ? t2 : ~t2) & ((v & 8) ? t3 : ~t3);
+                const uint32_t sel = (ssel ? alive : 0u) | (bsel ? ~alive : 0u);
+                r |= eq & sel;
+            }
+        }
+        return r;
+    }
+}
+
+// One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
+template <int RULE, int NP>
+__device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, uint32_t birth,
+                                             uint32_t survive)
+{
+    const Ends e = ends(x);
+    Pl<NP> s3, c3, y;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const uint32_t L = left_of(x, e, k), R = right_of(x, e, k);
+        s3.v[k] = lop3<kXor3>(L, x.v[k], R);
+        c3.v[k] = lop3<kMaj>(L, x.v[k], R);
+        y.v[k] = rule32_total<RULE>(st.ps.v[k], st.pc.v[k], st.cs.v[k], st.cc.v[k], s3.v[k],
+                                    c3.v[k], st.al.v[k], birth, survive);
+    }
+    st.ps = st.cs;
+    st.pc = st.cc;
+    st.cs = s3;
+    st.cc = c3;
+    st.al = x;
+    return y;
+}
+
+// Steps per block (rows prefetched ahead through the register ring): 8 for the
+// 2-plane kernels of depth >= 16, whose 2 waves/SIMD leave VGPRs to spare, 4
+// elsewhere (profiles/r01/ab_prefetch_depth.jsonl).  Host copy: prefetch_of().
+template <int NP, int K>
+constexpr int kPfOf()
+{
+    return (NP == 2 && K >= 16) ? 8 : 4;
+}
+
+// Code placement directive of a steady-state block (see the kernel): every
+// plane of the block's inputs passes through it.
+#define GOL_PL2(p) "+v"(x[p].v[0]), "+v"(x[p].v[1])
+#define GOL_PL4(p) "+v"(x[p].v[0]), "+v"(x[p].v[1]), "+v"(x[p].v[2]), "+v"(x[p].v[3])
+template <bool PAD, int NP, int PF>
+__device__ __forceinline__ void place_block(Pl<NP> (&x)[PF])
+{
+    static_assert((NP == 2 && (PF == 4 || PF == 8)) || (NP == 4 && PF == 4),
+                  "placement asm names 4 or 8 inputs");
+    if constexpr (NP == 2 && PF == 8) {
+        if constexpr (PAD)
+            asm volatile(".p2align 3\n\ts_nop 0"
+                         : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3), GOL_PL2(4), GOL_PL2(5),
+                           GOL_PL2(6), GOL_PL2(7) : : "memory");
+        else
+            asm volatile(".p2align 3"
+                         : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3), GOL_PL2(4), GOL_PL2(5),
+                           GOL_PL2(6), GOL_PL2(7) : : "memory");
+    } else if constexpr (NP == 2) {
+        if constexpr (PAD)
+            asm volatile(".p2align 3\n\ts_nop 0" : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3)
+                         : : "memory");
+        else
+            asm volatile(".p2align 3" : GOL_PL2(0), GOL_PL2(1), GOL_PL2(2), GOL_PL2(3) : : "memory");
+    } else {
+        if constexpr (PAD)
+            asm volatile(".p2align 3\n\ts_nop 0" : GOL_PL4(0), GOL_PL4(1), GOL_PL4(2), GOL_PL4(3)
+                         : : "memory");
+        else
+            asm volatile(".p2align 3" : GOL_PL4(0), GOL_PL4(1), GOL_PL4(2), GOL_PL4(3) : : "memory");
+    }
+}
+#undef GOL_PL2
+#undef GOL_PL4
+
+// Upper bound of a hand-off wait: polls of ~1 us each (the producer normally
+// finished its first rows long before), then give up, flag the error and go on
+// so that the launch always drains.
+constexpr int kPollLimit = 1 << 16;
+
+template <int K, int RULE, int NP, bool HAND>
+__global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
+{
+    constexpr bool kBirths = RULE != RULE_REF;
+    constexpr int G = NP / 2;  // words per lane group
+    constexpr int kPrefetch = kPfOf<NP, K>();
+    constexpr int kSideRows = 2 * (K - 1);  // hand-off rows per block: 2 per generation 1..K-1
+    static_assert(K + 2 * kPrefetch <= kGuardRows, "streaming loads must stay in the guard rows");
+    static_assert(!HAND || K >= kHandoffMinDepth, "hand-off kernels start at kHandoffMinDepth");
+    const int lane = threadIdx.x & 63;
+    const int64_t unit =
+        (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (unit >= a.total_units) return;
+
+    int sidx = 0;
+    for (int j = 1; j < a.nseg; ++j)
+        if (unit >= a.segs[j].unit0) sidx = j;
+    const SegDesc sg = a.segs[sidx];
+    const int64_t u = unit - sg.unit0;
+    // row blocks bottom-up: the block below (a hand-off producer) has the smaller index
+    const int64_t blk = sg.nblk - 1 - u / a.strips;
+    // strip `strip` of the row block lives in lanes [sub*L, sub*L + L); the DPP
+    // shifts cross from one strip into the next only at halo lanes
+    const int lshift = a.lane_shift;
+    const int L = 64 >> lshift;
+    const int sub = lane >> (6 - lshift);
+    const int lin = lane & (L - 1);
+    const int strip = (int)(u % a.strips) * (1 << lshift) + sub;
+
+    // lane group of this lane; its column mask (columns >= w are dead)
+    const int64_t q = (int64_t)strip * (L - 2) - 1 + lin;
+    const bool qin = (q >= 0) && (q < a.ng);
+    Pl<NP> cm;
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+        cm.v[k] = qin ? ((q == a.ng - 1) ? (uint32_t)(a.lastmask[k / 2] >> (32 * (k & 1))) : ~0u)
+                      : 0u;
+    const int64_t qc = qin ? q : 0;
+
+    const int64_t rb = sg.out_lo + blk * a.rows_per_wave;
+    const int64_t re = min(rb + a.rows_per_wave, sg.out_hi);
+    const int64_t T = (re - rb) + 2 * K;  // steps (input rows of a classic block)
+    const int64_t row_first = rb - K;     // local row of step 0
+    // hand-off roles: every block but the top one produces side rows for the block
+    // above; every block but the bottom one consumes those of the block below
+    const bool producer = HAND && blk > 0;
+    const bool consumer = HAND && blk < sg.nblk - 1;
+    // main loop bound: a consumer streams R + 2 input rows, then runs the tail
+    const int64_t t_main = consumer ? (re - rb) + 2 : T;
+
+    const uint64_t* inp = a.in + (sg.base_row + row_first) * a.stride + qc * G;
+    uint64_t* outp = a.out + (sg.base_row + rb) * a.stride + qc * G;
+    const bool st_lane = qin && lin >= 1 && lin <= L - 2;
+    uint64_t* my_side = HAND ? a.side + unit * a.side_slot + lane * G : nullptr;
+
+    // field-row validity of local row i (dead border) and buffer-row validity
+    const int64_t lo_ok = max((int64_t)0, -sg.glob0);             // first local row in field
+    const int64_t hi_ok = min(sg.in_rows, sg.field_h - sg.glob0);  // one past last
+
+    StageT<NP> st[K];
+#pragma unroll
+    for (int g = 0; g < K; ++g) st[g] = {};
+
+    Grp<NP> ring[kPrefetch];
+#pragma unroll
+    for (int p = 0; p < kPrefetch; ++p) ring[p] = load_grp<NP>(inp + (int64_t)p * a.stride);
+    const uint64_t* pf = inp + (int64_t)kPrefetch * a.stride;
+    int64_t pstride = a.stride;
+
+    // input row of step t: dead outside the field / buffer, columns >= w masked
+    auto ingest = [&](int64_t t, const Grp<NP>& xv) -> Pl<NP> {
+        const int64_t i = row_first + t;
+        const bool ok = (i >= lo_ok) && (i < hi_ok);
+        Pl<NP> x = planes_of(xv);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) x.v[k] = ok ? (x.v[k] & cm.v[k]) : 0u;
+        return x;
+    };
+    // stage g (generation g+1) at step t: emits local row row_first + t - (g+1)
+    auto stage = [&](int g, int64_t t, Pl<NP> x) -> Pl<NP> {
+        x = stage_step<RULE>(st[g], x, a.birth, a.survive);
+        if constexpr (kBirths) {
+            const int64_t r = sg.glob0 + row_first + t - (g + 1);  // field row
+            const bool rok = (r >= 0) && (r < sg.field_h);
+#pragma unroll
+            for (int k = 0; k < NP; ++k) x.v[k] = rok ? (x.v[k] & cm.v[k]) : 0u;
+        }
+        return x;
+    };
+    auto store = [&](int64_t t, const Pl<NP>& x) {
+        if (t >= 2 * K && t < T && st_lane)
+            *reinterpret_cast<Grp<NP>*>(outp + (t - 2 * K) * a.stride) = words_of(x);
+    };
+
+    // One block of kPrefetch steps from step t0.  GUARD (warm-up blocks): stage g
+    // first emits a row that can reach a valid output at step 2g+2 and needs the
+    // two ingests before it, so it only runs from step 2g on; skipping it earlier
+    // saves K*(K-1) of the 2K*K warm-up stage-steps.  In the warm-up blocks of a
+    // hand-off kernel, stage g's outputs at steps 2g+2 and 2g+3 (its first two rows,
+    // generation g+1) are also stored as side rows 2g and 2g+1 for the block above.
+    auto block = [&](int64_t t0, auto guard) {
+        constexpr bool kGuard = decltype(guard)::value;
+        Pl<NP> x[kPrefetch];
+#pragma unroll
+        for (int p = 0; p < kPrefetch; ++p) {
+            x[p] = ingest(t0 + p, ring[p]);
+            ring[p] = load_grp<NP>(pf);
+            pf += pstride;
+        }
+        // Code placement (steady-state blocks).  gfx950 issues this kernel's
+        // instruction mix (DPP move, v_alignbit, v_bitop3 chains; all 8-byte
+        // encodings) 10-25% faster when those instructions sit at addresses =
+        // 4 mod 8 with 2+ waves per SIMD, and faster at 0 mod 8 with one
+        // (profiles/r01/loop_alignment_ab.jsonl).  The scheduling barriers keep
+        // the 4-byte encodings (loads, ingest masks, SALU, stores) out of the
+        // compute, so one alignment directive places all of it; the compiler may
+        // add a hazard s_nop after it, so the 4-byte pad that gives the wanted
+        // parity is per kernel: loop_place.h, generated by tools/loop_align.py.
+        if constexpr (!kGuard) {
+            __builtin_amdgcn_sched_barrier(0);
+            place_block<life_loop_pad(K, RULE, NP, HAND) != 0, NP, kPrefetch>(x);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // stage g of step p only needs stage g-1 of step p and stage g of step
+        // p-1: issue the block's (p, g) pairs by anti-diagonal d = p + g so
+        // independent stage steps sit next to each other for the scheduler
+#pragma unroll
+        for (int d = 0; d < K + kPrefetch - 1; ++d) {
+#pragma unroll
+            for (int p = 0; p < kPrefetch; ++p) {
+                const int g = d - p;
+                if (g >= 0 && g < K && (!kGuard || t0 + p >= 2 * g)) {
+                    x[p] = stage(g, t0 + p, x[p]);
+                    if constexpr (HAND && kGuard) {
+                        if (g <= K - 2 && (t0 + p == 2 * g + 2 || t0 + p == 2 * g + 3))
+                            store_side<NP>(my_side + (int64_t)(t0 + p - 2) * 64 * G, x[p]);
+                    }
+                }
+            }
+        }
+        if constexpr (!kGuard) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < kPrefetch; ++p) store(t0 + p, x[p]);
+    };
+
+    // Warm-up blocks, unrolled (compile-time guards).
+    constexpr int kWarm = (2 * K + kPrefetch - 1) / kPrefetch * kPrefetch;
+    static_assert(!HAND || kWarm >= 2 * K, "side rows are all stored in the warm-up blocks");
+#pragma unroll
+    for (int t0 = 0; t0 < kWarm; t0 += kPrefetch) block(t0, std::true_type{});
+
+    if constexpr (HAND) {
+        // side rows 0..2K-3 stored: make them visible, then raise the flag
+        if (producer) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_store(a.flags + unit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+
+    // Steady state.  A consumer's last main block (t0 + kPrefetch == R + 2, the
+    // planner keeps R + 2 a multiple of kPrefetch) refills the ring with the
+    // block below's side rows: wait for its flag first.
+    for (int64_t t0 = kWarm; t0 < t_main; t0 += kPrefetch) {
+        if (HAND && consumer && t0 + kPrefetch == t_main) {
+            const uint32_t* f = a.flags + (unit - a.strips);
+            uint32_t v = 0;
+            for (int it = 0; it < kPollLimit; ++it) {
+                v = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT));
+                if (v) break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (lane == 0) {
+                if (!v) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // flags are all 0 between launches: reset the producer's
+                __hip_atomic_store(const_cast<uint32_t*>(f), 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            asm volatile("" ::: "memory");
+            pf = a.side + (unit - a.strips) * a.side_slot + lane * G;
+            pstride = 64 * G;
+        }
+        block(t0, std::false_type{});
+    }
+
+    if constexpr (HAND) {
+        if (consumer) {
+            // Tail: steps R+2+tau, tau = 0 .. 2K-3.  Side row tau (generation
+            // tau/2 + 1) enters at stage s0 = tau/2 + 1 in place of stage s0-1's
+            // output; stages below s0 are done (their rows are the block below's).
+            const int64_t tb = t_main;
+            auto tail = [&](int tau0) {  // tau0: a constant once the loop below is unrolled
+                Pl<NP> x[kPrefetch];
+#pragma unroll
+                for (int p = 0; p < kPrefetch; ++p) {
+                    x[p] = planes_of(ring[p]);
+                    if (tau0 + kPrefetch + p < kSideRows) {
+                        ring[p] = load_grp<NP>(pf);
+                        pf += pstride;
+                    }
+                }
+#pragma unroll
+                for (int d = 0; d < K + kPrefetch - 1; ++d) {
+#pragma unroll
+                    for (int p = 0; p < kPrefetch; ++p) {
+                        const int g = d - p, tau = tau0 + p;
+                        if (tau < kSideRows && g >= tau / 2 + 1 && g < K)
+                            x[p] = stage(g, tb + tau, x[p]);
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < kPrefetch; ++p)
+                    if (tau0 + p < kSideRows) store(tb + tau0 + p, x[p]);
+            };
+#pragma unroll
+            for (int tau0 = 0; tau0 < kSideRows; tau0 += kPrefetch) tail(tau0);
+        }
+    }
+}
+
+}  // namespace
+
+template <int K, int NP, bool HAND>
+hipError_t launch_kernel(const StepArgs& a, RuleKind rule, hipStream_t s)
+{
+    const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
+    const dim3 block(64 * kWavesPerBlock);
+    switch (rule) {
+    case RULE_REF:
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, NP, HAND>), grid, block, 0, s, a);
+        break;
+    case RULE_CONWAY:
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, NP, HAND>), grid, block, 0, s, a);
+        break;
+    default:
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, NP, HAND>), grid, block, 0, s, a);
+        break;
+    }
+    return hipGetLastError();
+}
+
+template <int K, int NP, bool HAND>
+int occupancy_kernel(RuleKind rule)
+{
+    int blocks = 0;
+    hipError_t e = hipErrorInvalidValue;
+    const int threads = 64 * kWavesPerBlock;
+    if (rule == RULE_REF)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, life_tb_kernel<K, RULE_REF, NP, HAND>, threads, 0);
+    else if (rule == RULE_CONWAY)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, life_tb_kernel<K, RULE_CONWAY, NP, HAND>, threads, 0);
+    else
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, life_tb_kernel<K, RULE_GENERIC, NP, HAND>, threads, 0);
+    return e == hipSuccess ? blocks : 0;
+}
+
+// 2-plane lane groups at every depth; 4-plane ones (dev build) up to depth 16,
+// where 5 planes x 4 x K state words still fit the register file.  Hand-off
+// kernels from kHandoffMinDepth on.
+constexpr bool depth_has_planes(int K, int NP) { return NP == 2 || (kDevKernels && NP == 4 && K <= 16); }
+
+template <int K>
+hipError_t launch_depth(const StepArgs& a, RuleKind rule, int planes, bool hand, hipStream_t s)
+{
+    if (hand && K < kHandoffMinDepth) return hipErrorInvalidValue;
+    if (planes == 4) {
+        if constexpr (depth_has_planes(K, 4)) {
+            if constexpr (K >= kHandoffMinDepth)
+                if (hand) return launch_kernel<K, 4, true>(a, rule, s);
+            return launch_kernel<K, 4, false>(a, rule, s);
+        }
+        return hipErrorInvalidValue;
+    }
+    if constexpr (K >= kHandoffMinDepth)
+        if (hand) return launch_kernel<K, 2, true>(a, rule, s);
+    return launch_kernel<K, 2, false>(a, rule, s);
+}
+
+template <int K>
+int occupancy_depth(RuleKind rule, int planes, bool hand)
+{
+    if (hand && K < kHandoffMinDepth) return 0;
+    if (planes == 4) {
+        if constexpr (depth_has_planes(K, 4)) {
+            if constexpr (K >= kHandoffMinDepth)
+                if (hand) return occupancy_kernel<K, 4, true>(rule);
+            return occupancy_kernel<K, 4, false>(rule);
+        }
+        return 0;
+    }
+    if constexpr (K >= kHandoffMinDepth)
+        if (hand) return occupancy_kernel<K, 2, true>(rule);
+    return occupancy_kernel<K, 2, false>(rule);
+}
+
+#define GOL_INSTANTIATE_DEPTH(K)                                                              \
+    template hipError_t launch_depth<K>(const StepArgs&, RuleKind, int, bool, hipStream_t);   \
+    template int occupancy_depth<K>(RuleKind, int, bool);
+
+}  // namespace gol

@@ -1,0 +1,8 @@
+// Stencil kernels of fused depth 20 (dev build only: make dev); see life_stencil.h.
+#include "life_stencil.h"
+
+#if GOL_DEV_KERNELS
+namespace gol {
+GOL_INSTANTIATE_DEPTH(20)
+}  // namespace gol
+#endif

@@ -1,0 +1,7 @@
+// Stencil kernels of fused depth 8 (all rule kinds, hand-off and classic row
+// blocks); see life_stencil.h.  One translation unit per depth keeps builds parallel.
+#include "life_stencil.h"
+
+namespace gol {
+GOL_INSTANTIATE_DEPTH(8)
+}  // namespace gol

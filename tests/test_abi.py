@@ -61,7 +61,8 @@ def test_rank_rows_rejects_bad_args(pkg):
 
 
 def test_bad_config_rejected_before_touching_gpu(pkg):
-    for kw in ({"rule": (512, 0)}, {"tb_depth": 3}):
+    for kw in ({"rule": (512, 0)}, {"tb_depth": 3}, {"handoff": 3}, {"tb_depth": 20},
+               {"word_planes": 4}, {"handoff": 2, "tb_depth": 2}):
         with pytest.raises(pkg.GolError) as ei:
             pkg.Engine(10, 10, **kw)
         assert ei.value.status == pkg.GOL_EINVAL
@@ -125,3 +126,15 @@ def test_four_plane_group_layout(tmp_path):
                     "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.stdout.strip() == "ok", r.returncode
+
+
+def test_shipped_library_has_only_product_kernels(pkg):
+    """The default build instantiates 2-plane stencil kernels of depths 1..16 only
+    (auto_layout's depths and the remainder launches); the 4-plane lane groups and
+    depths 20/24/32 live in the dev build (make dev)."""
+    blob = open(pkg.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"life_tb_kernelILi(\d+)ELi(\d)ELi(\d)ELb(\d)E", blob))
+    depths = {int(k) for k, _, _, _ in names}
+    assert depths == {1, 2, 4, 6, 7, 8, 12, 16}
+    assert {int(n) for _, _, n, _ in names} == {2}
+    assert {(int(k), int(h)) for k, _, _, h in names if int(h)} == {(k, 1) for k in (4, 6, 7, 8, 12, 16)}

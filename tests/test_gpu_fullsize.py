@@ -1,0 +1,68 @@
+"""GPU parity at the benchmark sizes (BASELINE.json configs[2..4]).
+
+The timed path itself: gol_create(65536, 65536) with defaults is the composite
+engine (2 same-device stripes on 2 streams, 256-row halo rounds, K = 16, hand-off
+row blocks) -- exactly what bench.py measures.  Checked
+  * against the CPU oracle after one step(16) call (the K = 16 kernel runs);
+  * after 600 more generations (two overlapped 256-generation rounds and a
+    partial one) against a streams=1, tb_depth=1, classic-block engine, which the
+    rest of the suite pins to the oracle at every size;
+  * the C4 stripe shapes (row stripes of 65536^2 over 2/4/8 with halo rounds),
+  * the C5 per-GPU unit (32768 x 262144) against the oracle.
+Bit-exact (integer work): digests (live count + order-independent 64-bit hash)
+must be equal.
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = 65536
+THREADS = 16
+
+
+def digest_of(pkg, h, w, rule, gens, seed=1, **kw):
+    with pkg.Engine(h, w, rule=rule, device=0, **kw) as e:
+        e.init_random(seed)
+        if gens:
+            e.step(gens)
+        return e.digest()
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+def test_c3_default_engine_vs_oracle_and_depth1(pkg, oracle, rule):
+    R = oracle.REF_RULE if rule == "ref" else oracle.CONWAY
+    with pkg.Engine(N, N, rule=R, device=0) as e:
+        assert e.tb_depth == 16 and e.handoff, (e.tb_depth, e.handoff)
+        e.init_random(1)
+        e.step(16)  # one full-depth launch per stripe
+        d16 = e.digest()
+        e.step(600)  # 2 overlapped 256-generation rounds + a partial one
+        d616 = e.digest()
+    g = oracle.bp_run(oracle.bp_random(N, N, 1), N, 16, R, threads=THREADS)
+    assert d16 == oracle.bp_digest(g, N)
+    del g
+    assert d616 == digest_of(pkg, N, N, R, 616, streams=1, tb_depth=1)
+
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_c4_stripes_equal_single_field(pkg, nranks):
+    """C4 partition: 65536^2 in `nranks` row stripes (gol_rank_rows), default K and
+    halo depth (8K = 128), 3 rounds + a partial one, overlapped exchanges."""
+    gens = 3 * 128 + 40
+    want = digest_of(pkg, N, N, pkg.CONWAY, gens, seed=4)
+    with pkg.Group(N, N, nranks, rule=pkg.CONWAY) as grp:
+        m = grp.members[0]
+        assert (m.tb_depth, m.halo_depth) == (16, 128)
+        grp.init_random(4)
+        grp.step(gens)
+        assert grp.digest() == want
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+def test_c5_per_gpu_unit_vs_oracle(pkg, oracle, rule):
+    """The C5 weak-scaling unit (262144^2 over 8 GPUs = 32768 x 262144 per GPU)."""
+    h, w = 32768, 262144
+    R = oracle.REF_RULE if rule == "ref" else oracle.CONWAY
+    got = digest_of(pkg, h, w, R, 16)
+    g = oracle.bp_run(oracle.bp_random(h, w, 1), w, 16, R, threads=THREADS)
+    assert got == oracle.bp_digest(g, w)

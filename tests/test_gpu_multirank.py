@@ -22,20 +22,20 @@ def test_group_matches_single_field(pkg, oracle, nranks, rule):
     R = {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}[rule]
     h, w = 203, 4000
     g = oracle.bp_random(h, w, 3 + nranks)
-    for tb, hx, gens, kv, lanes, wp in ((8, 0, 37, 1, 0, 0), (4, 12, 30, 1, 0, 0),
-                                        (2, 5, 11, 1, 0, 0), (1, 3, 7, 1, 0, 0),
-                                        (16, 16, 33, 1, 0, 0), (8, 0, 37, 2, 0, 0),
-                                        (16, 24, 50, 2, 0, 0), (16, 0, 70, 1, 32, 0),
-                                        (8, 0, 37, 1, 16, 0), (8, 0, 37, 1, 0, 2),
-                                        (16, 0, 40, 1, 0, 4)):
+    for tb, hx, gens, ho, lanes, rpw in ((8, 0, 37, 0, 0, 0), (4, 12, 30, 0, 0, 0),
+                                         (2, 5, 11, 0, 0, 0), (1, 3, 7, 0, 0, 0),
+                                         (16, 16, 33, 0, 0, 0), (8, 0, 37, 1, 0, 0),
+                                         (16, 24, 50, 1, 0, 0), (16, 0, 70, 0, 32, 0),
+                                         (8, 0, 37, 0, 16, 0), (8, 0, 37, 2, 0, 18),
+                                         (16, 0, 40, 2, 0, 38), (4, 16, 45, 2, 0, 10)):
         ref = oracle.bp_run(g, w, gens, R)
-        with pkg.Group(h, w, nranks, rule=R, tb_depth=tb, halo_depth=hx,
-                       kernel_variant=kv, strip_lanes=lanes, word_planes=wp) as grp:
+        with pkg.Group(h, w, nranks, rule=R, tb_depth=tb, halo_depth=hx, handoff=ho,
+                       strip_lanes=lanes, rows_per_wave=rpw) as grp:
             grp.load_packed(g)
             grp.step(gens)
             grp.sync()
             got = grp.store_packed()
-            assert (got == ref).all(), f"tb {tb} hx {hx} gens {gens}"
+            assert (got == ref).all(), f"tb {tb} hx {hx} gens {gens} handoff {ho}"
             assert grp.digest() == oracle.bp_digest(ref, w)
 
 
@@ -55,7 +55,8 @@ def test_group_reference_data(pkg, ref_data):
 
 
 def test_group_large_equals_single(pkg):
-    """Size-independent property at the per-GPU shape of 8-way 65536^2 runs."""
+    """Size-independent property: 8 stripes of 2048 rows (hand-off row blocks,
+    overlapped rounds) equal the single field."""
     h, w = 16384, 65536
     with pkg.Engine(h, w, rule=pkg.CONWAY, device=0) as e:
         e.init_random(9)
@@ -141,3 +142,38 @@ def test_group_overlap_uneven_stripes(pkg, oracle):
         for _ in range(3):
             grp.step(16)
         assert (grp.store_packed() == oracle.bp_run(g, w, 48, oracle.CONWAY)).all()
+
+
+@pytest.mark.parametrize("kind", ["group", "composite"])
+def test_store_and_digest_without_sync_after_overlap(pkg, oracle, kind):
+    """The last launch of an overlapped round writes the band rows on a second
+    stream; store/digest right after gol_step (no gol_sync) must still see them.
+    A Conway field keeps changing, so stale band rows would show."""
+    h, w = 2000, 3000
+    g = oracle.bp_random(h, w, 99)
+    want = oracle.bp_run(g, w, 96, oracle.CONWAY)
+    if kind == "group":
+        eng = pkg.Group(h, w, 2, rule=pkg.CONWAY, tb_depth=8, halo_depth=32)
+    else:
+        eng = pkg.Engine(h, w, rule=pkg.CONWAY, device=0, streams=2, tb_depth=8, halo_depth=32)
+    with eng:
+        eng.load_packed(g)
+        eng.step(96)  # 3 full rounds: ends with a band launch + overlapped exchange
+        assert eng.digest() == oracle.bp_digest(want, w)
+        eng.step(96)
+        assert (eng.store_packed() == oracle.bp_run(want, w, 96, oracle.CONWAY)).all()
+
+
+def test_group_reload_one_member(pkg, oracle):
+    """A member reloaded after an overlapped step (its halos cleared) makes the next
+    round exchange afresh for every member."""
+    h, w = 600, 700
+    g = oracle.bp_random(h, w, 5)
+    with pkg.Group(h, w, 3, rule=pkg.CONWAY, tb_depth=4, halo_depth=16) as grp:
+        grp.load_packed(g)
+        grp.step(32)
+        mid = oracle.bp_run(g, w, 32, oracle.CONWAY)
+        m = grp.members[1]
+        m.load_packed(mid[m.row0:m.row0 + m.rows])  # same rows, halos now stale
+        grp.step(48)
+        assert (grp.store_packed() == oracle.bp_run(mid, w, 48, oracle.CONWAY)).all()

@@ -17,15 +17,8 @@ pytestmark = pytest.mark.gpu
 
 GOLD = json.load(open(os.path.join(GOLDEN, "ref_outputs.json")))
 H, W = GOLD["h"], GOLD["w"]
-DEPTHS = [1, 2, 4, 6, 7, 8, 12, 16, 20, 24, 32]
-
-
-def has_kernel(depth, variant, planes):
-    """Instantiated stencil kernels (life_kernels.hip has_kernel; `variant` is
-    gol_config.kernel_variant: 2 = neighbour-sum state)."""
-    if planes == 2:
-        return variant != 2 or depth <= 16
-    return depth <= 16 and (variant != 2 or depth <= 8)
+DEPTHS = [1, 2, 4, 6, 7, 8, 12, 16]  # the shipped library's fused depths
+HAND_DEPTHS = [d for d in DEPTHS if d >= 4]  # depths with hand-off row blocks
 
 
 def mask(ns):
@@ -64,15 +57,19 @@ def test_reference_1000_generations(pkg, ref_data):
 
 @pytest.mark.parametrize("depth", DEPTHS)
 def test_reference_per_generation(pkg, oracle, ref_data, depth):
-    """Gens 1..8 one at a time and in one call, at every fused depth (the B/S2
-    field reaches a fixed point after ~5 gens, so early gens matter)."""
-    g = oracle.bp_pack(ref_data, H, W)
+    """Gens 1..8 and 12, 16 at every fused depth, each count reached by ONE
+    gol_step(g) call on a fresh load, so the fused kernel of that depth (and the
+    remainder depths pick_depth chooses) really runs (the B/S2 field reaches a
+    fixed point after ~5 gens, so the early gens carry the information)."""
+    g0 = oracle.bp_pack(ref_data, H, W)
+    want = {0: g0}
+    for gen in range(1, 17):
+        want[gen] = oracle.bp_run(want[gen - 1], W, 1)
     with pkg.Engine(H, W, device=0, tb_depth=depth) as e:
-        e.load_ascii(ref_data)
-        for gen in range(1, 9):
-            e.step(1)
-            g = oracle.bp_run(g, W, 1)
-            assert (e.store_packed() == g).all(), f"gen {gen}"
+        for gens in (1, 2, 3, 4, 5, 6, 7, 8, 12, 16):
+            e.load_ascii(ref_data)
+            e.step(gens)
+            assert (e.store_packed() == want[gens]).all(), f"depth {depth} gens {gens}"
 
 
 # ------------------------------------------------- random fields, all rules
@@ -90,57 +87,94 @@ def test_random_fields_every_depth(pkg, oracle, shape, rule):
     g = oracle.bp_random(h, w, seed)
     for gens in (1, 3, 16, 21, 70):
         want[gens] = oracle.bp_run(g, w, gens, R)
-    for depth, variant, planes in [(d, v, p) for d in DEPTHS for v in (1, 2, 3) for p in (2, 4)
-                                   if has_kernel(d, v, p)]:
-        for gens, ref in want.items():
-            with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth,
-                            kernel_variant=variant, word_planes=planes) as e:
-                assert e.word_planes == planes
-                e.init_random(seed)
-                e.step(gens)
-                got = e.store_packed()
-                assert (got == ref).all(), f"depth {depth} variant {variant} planes {planes} gens {gens}"
-                assert e.digest() == oracle.bp_digest(ref, w)
+    for depth in DEPTHS:
+        for handoff in ((1, 2) if depth >= 4 else (1,)):
+            with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth, handoff=handoff) as e:
+                for gens, ref in want.items():
+                    e.init_random(seed)
+                    e.step(gens)
+                    got = e.store_packed()
+                    assert (got == ref).all(), f"depth {depth} handoff {handoff} gens {gens}"
+                    assert e.digest() == oracle.bp_digest(ref, w)
 
 
-@pytest.mark.parametrize("planes", [2, 4])
 @pytest.mark.parametrize("lanes", [64, 32, 16])
 @pytest.mark.parametrize("rule", ["ref", "conway", "daynight"])
-def test_strip_widths(pkg, oracle, lanes, rule, planes):
+def test_strip_widths(pkg, oracle, lanes, rule):
     """Narrow strips (32/16 lanes, 2/4 per wavefront): strip seams inside a
-    wavefront, partial last strip groups, every depth class, both lane-group
-    layouts (odd word counts leave the last 4-plane group half empty)."""
+    wavefront, partial last strip groups, every depth class."""
     R = rules(oracle)[rule]
     for h, w in [(1, 1), (7, 65), (40, 1921), (33, 1983), (129, 4097), (64, 900), (9, 3969)]:
         seed = 7 * h + w
         g = oracle.bp_random(h, w, seed)
-        for depth in (1, 4, 16, 32):
-            if not has_kernel(depth, 1, planes):
-                continue
+        for depth in (1, 4, 8, 16):
             for gens in (3, 33, 70):
                 ref = oracle.bp_run(g, w, gens, R)
-                with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth, strip_lanes=lanes,
-                                word_planes=planes) as e:
-                    assert e.strip_lanes == lanes and e.word_planes == planes
+                with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth, strip_lanes=lanes) as e:
+                    assert e.strip_lanes == lanes
                     e.init_random(seed)
                     e.step(gens)
                     assert (e.store_packed() == ref).all(), f"{h}x{w} depth {depth} gens {gens}"
 
 
-@pytest.mark.parametrize("rpw", [16, 32, 48, 100])
-@pytest.mark.parametrize("variant", [1, 2, 3])
-def test_row_blocking(pkg, oracle, rpw, variant):
-    """Many row blocks per strip (rows_per_wave small): block seams exact."""
+@pytest.mark.parametrize("rpw", [14, 16, 30, 32, 46, 48, 100])
+@pytest.mark.parametrize("handoff", [1, 2])
+def test_row_blocking(pkg, oracle, rpw, handoff):
+    """Many row blocks per strip (rows_per_wave small): block seams exact, both
+    block closures.  Hand-off needs R + 2 to be a whole number of prefetch blocks
+    (4 steps at depth 8) and at least the 16 warm-up steps + one block: 30 and 46
+    hand over, the others fall back to classic blocks."""
     h, w = 300, 4100
     g = oracle.bp_random(h, w, 5)
     ref = oracle.bp_run(g, w, 16, oracle.CONWAY)
     for lanes in (64, 32, 16):
-        for planes in (2, 4):
-            with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw,
-                            kernel_variant=variant, strip_lanes=lanes, word_planes=planes) as e:
-                e.init_random(5)
-                e.step(16)
-                assert (e.store_packed() == ref).all(), (lanes, planes)
+        with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw,
+                        handoff=handoff, strip_lanes=lanes) as e:
+            assert e.handoff == (handoff == 2 and (rpw + 2) % 4 == 0 and rpw + 2 >= 20)
+            e.init_random(5)
+            e.step(16)
+            assert (e.store_packed() == ref).all(), (lanes, rpw)
+
+
+@pytest.mark.parametrize("depth", HAND_DEPTHS)
+@pytest.mark.parametrize("rule", ["ref", "conway", "highlife"])
+def test_handoff_seams(pkg, oracle, depth, rule):
+    """Hand-off row blocks at every depth: the shortest legal rows_per_wave (most
+    seams per strip), partial last blocks (h not a multiple of R), births at the
+    seams (Conway / HighLife), odd widths, and remainder launches of smaller
+    depth in the same call.  Must equal the oracle and the classic blocks."""
+    R = rules(oracle)[rule]
+    pf = 8 if depth >= 16 else 4
+    warm = -(-2 * depth // pf) * pf
+    rpw = warm + pf - 2
+    for h, w in ((5 * rpw + 3, 130), (3 * rpw, 4100), (2 * rpw + 1, 63)):
+        g = oracle.bp_random(h, w, h + depth)
+        for gens in (depth, 3 * depth + 5):
+            ref = oracle.bp_run(g, w, gens, R)
+            for handoff in (1, 2):
+                with pkg.Engine(h, w, rule=R, device=0, tb_depth=depth, rows_per_wave=rpw,
+                                handoff=handoff, streams=1) as e:
+                    assert e.handoff == (handoff == 2)
+                    e.load_packed(g)
+                    e.step(gens)
+                    assert (e.store_packed() == ref).all(), (h, w, gens, handoff)
+
+
+def test_handoff_repeated_launches_and_graphs(pkg, oracle):
+    """Hand-off flags are reset by every consumer, so back-to-back launches, graph
+    replays and alternating call sizes (different remainder depths) stay exact."""
+    h, w = 1000, 3000
+    g = oracle.bp_random(h, w, 77)
+    with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, tb_depth=16, rows_per_wave=38,
+                    handoff=2, streams=1) as e:
+        assert e.handoff
+        e.load_packed(g)
+        total = 0
+        for gens in (64, 64, 37, 64, 37, 5, 100):
+            e.step(gens)
+            total += gens
+        e.sync()
+        assert (e.store_packed() == oracle.bp_run(g, w, total, oracle.CONWAY)).all()
 
 
 def test_load_packed_roundtrip(pkg, oracle):
@@ -172,9 +206,15 @@ def test_ascii_roundtrip_and_errors(pkg, oracle):
     with pytest.raises(pkg.GolError):
         pkg.Engine(5, 5, device=0, tb_depth=3)
     with pytest.raises(pkg.GolError):
-        pkg.Engine(5, 5, device=0, tb_depth=20, word_planes=4)
+        pkg.Engine(5, 5, device=0, tb_depth=20)  # dev build only
+    with pytest.raises(pkg.GolError):
+        pkg.Engine(5, 5, device=0, word_planes=4)  # dev build only
     with pytest.raises(pkg.GolError):
         pkg.Engine(5, 5, device=0, word_planes=3)
+    with pytest.raises(pkg.GolError):
+        pkg.Engine(5, 5, device=0, handoff=3)
+    with pytest.raises(pkg.GolError):
+        pkg.Engine(5, 5, device=0, handoff=2, tb_depth=2)
 
 
 @pytest.mark.parametrize("P", [2, 3, 5, 8])
@@ -207,51 +247,40 @@ def test_generic_rules(pkg, oracle, rule):
 # ------------------------------------------------------------ C2: 4096^2
 @pytest.mark.parametrize("rule", ["ref", "conway"])
 def test_c2_4096_per_generation(pkg, oracle, rule):
+    """The default C2 engine (K = 8): every checked generation count reached by one
+    gol_step call from the initial field, so the depth-8 kernel and the remainder
+    depths run, plus gens 1..16 one call each for the early B/S2 generations."""
     h = w = 4096
     R = rules(oracle)[rule]
-    g = oracle.bp_random(h, w, 1)
+    g0 = oracle.bp_random(h, w, 1)
+    want = {0: g0}
+    for gen in range(1, 41):
+        want[gen] = oracle.bp_run(want[gen - 1], w, 1, R, threads=16)
     with pkg.Engine(h, w, rule=R, device=0) as e:
         e.init_random(1)
-        assert (e.store_packed() == g).all()
+        assert (e.store_packed() == g0).all()
+        for gens in (1, 2, 3, 5, 8, 9, 13, 16, 24, 40):
+            e.init_random(1)
+            e.step(gens)
+            assert e.digest() == oracle.bp_digest(want[gens], w), f"gens {gens}"
+        e.init_random(1)
         for gen in range(1, 17):
             e.step(1)
-            g = oracle.bp_run(g, w, 1, R, threads=16)
-            assert e.digest() == oracle.bp_digest(g, w), f"gen {gen}"
-        assert (e.store_packed() == g).all()
+            assert e.digest() == oracle.bp_digest(want[gen], w), f"gen {gen} (one at a time)"
+        assert (e.store_packed() == want[16]).all()
 
 
 def test_c2_4096_1000_generations_depths_agree(pkg):
-    """Size-independent property: every fused depth gives the same field."""
+    """Size-independent property: every fused depth, both block closures, gives
+    the same field after 1000 Conway generations."""
     digests = set()
     for depth in DEPTHS:
-        with pkg.Engine(4096, 4096, rule=(1 << 3, 12), device=0, tb_depth=depth) as e:
-            e.init_random(1)
-            e.step(1000)
-            digests.add(e.digest())
-    assert len(digests) == 1
-
-
-# ------------------------------------------------------------ C3: 65536^2
-@pytest.mark.slow
-def test_c3_65536_vs_oracle(pkg, oracle):
-    h = w = 65536
-    with pkg.Engine(h, w, rule=oracle.CONWAY, device=0) as e:
-        e.init_random(1)
-        e.step(3)
-        got = e.digest()
-    g = oracle.bp_random(h, w, 1)
-    g = oracle.bp_run(g, w, 3, oracle.CONWAY, threads=16)
-    assert got == oracle.bp_digest(g, w)
-
-
-@pytest.mark.slow
-def test_c3_65536_depths_agree(pkg):
-    digests = set()
-    for depth in (1, 8, 16, 32):
-        with pkg.Engine(65536, 65536, rule=(1 << 3, 12), device=0, tb_depth=depth) as e:
-            e.init_random(2)
-            e.step(48)
-            digests.add(e.digest())
+        for handoff in ((1, 2) if depth >= 4 else (1,)):
+            with pkg.Engine(4096, 4096, rule=(1 << 3, 12), device=0, tb_depth=depth,
+                            handoff=handoff) as e:
+                e.init_random(1)
+                e.step(1000)
+                digests.add(e.digest())
     assert len(digests) == 1
 
 
@@ -281,14 +310,13 @@ def test_timing_sampled(pkg):
 @pytest.mark.parametrize("w", [4100, 4033])
 def test_ascii_codec_large_and_malformed(pkg, oracle, w):
     """Device ASCII codec (ballot pack / coalesced unpack) on multi-word rows (odd
-    and even word counts), both lane-group layouts, and a malformed line deep
+    and even word counts), single and composite engines, and a malformed line deep
     inside the field."""
     h = 333
     g = oracle.bp_random(h, w, 31)
     data = oracle.bp_unpack(g, w)
-    for streams, planes in ((1, 2), (2, 2), (1, 4), (2, 4)):
-        with pkg.Engine(h, w, device=0, streams=streams, rule=pkg.CONWAY,
-                        word_planes=planes) as e:
+    for streams in (1, 2):
+        with pkg.Engine(h, w, device=0, streams=streams, rule=pkg.CONWAY) as e:
             e.load_ascii(data)
             assert (e.store_packed() == g).all()
             assert e.store_ascii() == data
