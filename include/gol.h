@@ -98,7 +98,9 @@ typedef struct gol_timing {
     uint64_t launches;     /* stencil kernel launches timed (sampled) */
     double kernel_ms;      /* sum of their HIP-event durations */
     double cell_gens;      /* cell-generations those launches produced (own rows) */
-    double cell_gens_computed; /* including redundant halo/overlap work */
+    double cell_gens_computed; /* what the lanes process: including the vertical
+                                  halo stage-rows of classic blocks and the
+                                  strips' halo lanes */
     uint32_t streams;      /* stripe streams whose launches run concurrently */
     uint32_t reserved;
 } gol_timing;

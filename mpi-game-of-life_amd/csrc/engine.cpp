@@ -277,16 +277,12 @@ int32_t strip_groups(uint64_t wq, int shift)
     return (int32_t)((strips + per - 1) / per);
 }
 
-// Hand-off constraints on the rows per wavefront R of a launch of depth d: a
-// consumer streams R + 2 input rows in whole prefetch blocks after the warm-up
-// blocks (life_stencil.h), so R + 2 is a multiple of the prefetch block and
-// R + 2 >= warm-up + one block.
-bool handoff_fits(int64_t R, int d, int planes)
-{
-    if (d < gol::kHandoffMinDepth) return false;
-    const int pf = gol::prefetch_of(d, planes);
-    return (R + 2) % pf == 0 && R + 2 >= gol::warm_steps_of(d, planes) + pf;
-}
+// Hand-off constraint on the rows per wavefront R of a launch of depth d
+// (gol::handoff_toff): a consumer block streams R + 2 input rows, kernels exist
+// for two alignments of that count to the prefetch blocks, and the refill that
+// first fetches side rows (the flag wait sits in front of it) must come after the
+// unrolled warm-up blocks.
+bool handoff_fits(int64_t R, int d, int planes) { return gol::handoff_toff(R, d, planes) >= 0; }
 
 // Rows per wavefront and strip width for one launch plan.  Every wavefront of
 // a launch does about the same work, so the launch time is set by the most
@@ -732,6 +728,7 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         a.flags = e->flags[region];
         a.err = e->d_err;
         a.side_slot = (int64_t)2 * (depth - 1) * 64 * (e->planes / 2);
+        a.tail_off = gol::handoff_toff(p.rpw, (int)depth, e->planes);
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = e->timing_every && (e->launch_count++ % e->timing_every) == 0;
@@ -745,10 +742,19 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     if (timed) {
         HIP_TRY(hipEventRecord(e1, s));
         e->ev_pending.push_back({e0, e1});
+        // cell-generations the lanes actually process: every stage of a block
+        // computes its rows, a classic block (and the last block of a hand-off
+        // segment) also d(d-1) stage-rows of vertical halo, and every strip also
+        // its 2 halo lanes
         double comp = 0;
-        for (const auto& sg : p.segs) comp += (double)(sg.out_hi - sg.out_lo);
+        for (const auto& sg : p.segs) {
+            const double n = (double)std::max<int64_t>(0, sg.out_hi - sg.out_lo);
+            const double classic = hand ? (double)std::min<int64_t>(1, sg.nblk) : (double)sg.nblk;
+            comp += depth * n + classic * depth * (depth - 1.0);
+        }
+        const double cols = (double)p.groups * 64.0 * 32.0 * e->planes;
         e->pending_cells.push_back(p.own_rows * (double)e->W * depth);
-        e->pending_cells_comp.push_back(comp * (double)e->W * depth);
+        e->pending_cells_comp.push_back(comp * cols);
     }
     if (swap) e->cur ^= 1;
     return GOL_OK;

@@ -55,7 +55,7 @@ struct StepArgs {
     int32_t nseg;
     int32_t strips;       // strip groups per row: ceil(ceil(wq / (L-2)) / (64/L))
     int32_t lane_shift;   // L = 64 >> lane_shift lanes per strip (0, 1 or 2)
-    int32_t pad0;
+    int32_t tail_off;     // hand-off kernels: (R + 2 - warm-up) mod prefetch block
     int64_t stride;       // words per buffer row
     int64_t ng;           // lane groups per field row = ceil(ceil(w / 64) / (NP/2))
     uint64_t lastmask[2]; // stored-form valid bits of the last group's words
@@ -92,6 +92,18 @@ constexpr int prefetch_of(int K, int planes) { return (planes == 2 && K >= 16) ?
 constexpr int warm_steps_of(int K, int planes)
 {
     return (2 * K + prefetch_of(K, planes) - 1) / prefetch_of(K, planes) * prefetch_of(K, planes);
+}
+// Hand-off kernels exist for tail offsets 0 and prefetch/2: a consumer block of R
+// rows streams R + 2 input steps after the warm-up, i.e. (R + 2 - warm) mod
+// prefetch must be one of them, and at least one whole block must precede the
+// tail.  Returns the offset, or -1 if R does not fit.
+constexpr int handoff_toff(int64_t R, int K, int planes)
+{
+    const int pf = prefetch_of(K, planes), warm = warm_steps_of(K, planes);
+    if (K < kHandoffMinDepth || R + 2 < warm + pf) return -1;
+    const int off = (int)((R + 2 - warm) % pf);
+    if (off != 0 && off != pf / 2) return -1;
+    return R + 2 - off >= warm + pf ? off : -1;
 }
 
 // Launch `depth` fused generations (depth in kDepthList) on lane groups of

@@ -50,6 +50,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <climits>
 #include <type_traits>
 
 #include "bitlayout.h"
@@ -299,7 +300,7 @@ __device__ __forceinline__ void place_block(Pl<NP> (&x)[PF])
 // so that the launch always drains.
 constexpr int kPollLimit = 1 << 16;
 
-template <int K, int RULE, int NP, bool HAND>
+template <int K, int RULE, int NP, bool HAND, int TOFF>
 __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 {
     constexpr bool kBirths = RULE != RULE_REF;
@@ -308,6 +309,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     constexpr int kSideRows = 2 * (K - 1);  // hand-off rows per block: 2 per generation 1..K-1
     static_assert(K + 2 * kPrefetch <= kGuardRows, "streaming loads must stay in the guard rows");
     static_assert(!HAND || K >= kHandoffMinDepth, "hand-off kernels start at kHandoffMinDepth");
+    static_assert(TOFF >= 0 && TOFF < kPrefetch && (HAND || TOFF == 0), "tail offset");
     const int lane = threadIdx.x & 63;
     const int64_t unit =
         (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -326,71 +328,95 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     const int L = 64 >> lshift;
     const int sub = lane >> (6 - lshift);
     const int lin = lane & (L - 1);
-    const int strip = (int)(u % a.strips) * (1 << lshift) + sub;
-
-    // lane group of this lane; its column mask (columns >= w are dead)
-    const int64_t q = (int64_t)strip * (L - 2) - 1 + lin;
+    // lane group of this lane: q = qbase + sub*(L-2) + lin, qbase (uniform) the
+    // group one left of the wave's first strip; its column mask (columns >= w dead)
+    const int64_t qbase = (u % a.strips) * (int64_t)(1 << lshift) * (L - 2) - 1;
+    const int64_t q = qbase + sub * (L - 2) + lin;
     const bool qin = (q >= 0) && (q < a.ng);
     Pl<NP> cm;
 #pragma unroll
     for (int k = 0; k < NP; ++k)
         cm.v[k] = qin ? ((q == a.ng - 1) ? (uint32_t)(a.lastmask[k / 2] >> (32 * (k & 1))) : ~0u)
                       : 0u;
-    const int64_t qc = qin ? q : 0;
+    // lanes outside the field read the strip's first group (any word of the row
+    // will do; masked to 0); qc - qbase is in [0, 64) on every lane, which is how
+    // the lanes index a 64-entry side row
+    const int64_t qc = qin ? q : qbase + 1;
+    // Every access = a uniform row base (SGPRs) + this per-lane byte offset.
+    const uint32_t voff = (uint32_t)(qc * G * 8);
 
     const int64_t rb = sg.out_lo + blk * a.rows_per_wave;
     const int64_t re = min(rb + a.rows_per_wave, sg.out_hi);
-    const int64_t T = (re - rb) + 2 * K;  // steps (input rows of a classic block)
-    const int64_t row_first = rb - K;     // local row of step 0
+    // step counts and indices are 32-bit (a block has at most rows_per_wave + 2K
+    // steps): uniform 32-bit compares stay on the scalar unit, 64-bit ones do not
+    const int32_t T = (int32_t)(re - rb) + 2 * K;  // steps (input rows of a classic block)
+    const int64_t row_first = rb - K;              // local row of step 0
     // hand-off roles: every block but the top one produces side rows for the block
     // above; every block but the bottom one consumes those of the block below
     const bool producer = HAND && blk > 0;
     const bool consumer = HAND && blk < sg.nblk - 1;
-    // main loop bound: a consumer streams R + 2 input rows, then runs the tail
-    const int64_t t_main = consumer ? (re - rb) + 2 : T;
+    // a consumer streams R + 2 input rows (steps < t_side), then side rows
+    const int32_t t_side = consumer ? (int32_t)(re - rb) + 2 : INT32_MAX;
 
-    const uint64_t* inp = a.in + (sg.base_row + row_first) * a.stride + qc * G;
-    uint64_t* outp = a.out + (sg.base_row + rb) * a.stride + qc * G;
+    const char* in_rows = reinterpret_cast<const char*>(a.in + (sg.base_row + row_first) * a.stride);
+    char* out_rows = reinterpret_cast<char*>(a.out + (sg.base_row + rb) * a.stride);
+    const int64_t row_bytes = a.stride * 8;
+    constexpr int64_t kSideRowBytes = 64 * G * 8;
+    // slot bases shifted by qbase so that slot entry (qc - qbase) is at base + voff
+    char* my_side = HAND ? reinterpret_cast<char*>(a.side + unit * a.side_slot - qbase * G) : nullptr;
+    const char* dn_side =
+        HAND ? reinterpret_cast<const char*>(a.side + (unit - a.strips) * a.side_slot - qbase * G)
+             : nullptr;
     const bool st_lane = qin && lin >= 1 && lin <= L - 2;
-    uint64_t* my_side = HAND ? a.side + unit * a.side_slot + lane * G : nullptr;
 
-    // field-row validity of local row i (dead border) and buffer-row validity
-    const int64_t lo_ok = max((int64_t)0, -sg.glob0);             // first local row in field
-    const int64_t hi_ok = min(sg.in_rows, sg.field_h - sg.glob0);  // one past last
+    // field-row validity of the row of step t (dead border) and buffer-row validity:
+    // steps [t_lo, t_hi) read rows inside both
+    const int32_t t_lo = (int32_t)(max((int64_t)0, -sg.glob0) - row_first);
+    const int32_t t_hi = (int32_t)(min(sg.in_rows, sg.field_h - sg.glob0) - row_first);
+    // field rows of stage outputs: stage g at step t emits field row
+    // glob0 + row_first + t - (g+1), alive only in [0, field_h)
+    const int32_t f_lo = (int32_t)(-(sg.glob0 + row_first));
+    const int32_t f_hi = (int32_t)(sg.field_h - (sg.glob0 + row_first));
 
     StageT<NP> st[K];
 #pragma unroll
     for (int g = 0; g < K; ++g) st[g] = {};
 
+    // the row streamed at step s: input row row_first + s, or for a consumer from
+    // step t_side on the block below's side row s - t_side (uniform select)
+    auto load_step = [&](int32_t s) -> Grp<NP> {
+        const char* base = s < t_side ? in_rows + (int64_t)s * row_bytes
+                                      : dn_side + (int64_t)(s - t_side) * kSideRowBytes;
+        return load_grp<NP>(reinterpret_cast<const uint64_t*>(base + voff));
+    };
     Grp<NP> ring[kPrefetch];
 #pragma unroll
-    for (int p = 0; p < kPrefetch; ++p) ring[p] = load_grp<NP>(inp + (int64_t)p * a.stride);
-    const uint64_t* pf = inp + (int64_t)kPrefetch * a.stride;
-    int64_t pstride = a.stride;
+    for (int p = 0; p < kPrefetch; ++p) ring[p] = load_step(p);
 
-    // input row of step t: dead outside the field / buffer, columns >= w masked
-    auto ingest = [&](int64_t t, const Grp<NP>& xv) -> Pl<NP> {
-        const int64_t i = row_first + t;
-        const bool ok = (i >= lo_ok) && (i < hi_ok);
+    // row of step t: an input row is dead outside the field / buffer; a side row
+    // comes as the block below computed it; columns >= w masked
+    auto ingest = [&](int32_t t, const Grp<NP>& xv) -> Pl<NP> {
+        const bool ok = t >= t_side || ((t >= t_lo) && (t < t_hi));
         Pl<NP> x = planes_of(xv);
 #pragma unroll
         for (int k = 0; k < NP; ++k) x.v[k] = ok ? (x.v[k] & cm.v[k]) : 0u;
         return x;
     };
     // stage g (generation g+1) at step t: emits local row row_first + t - (g+1)
-    auto stage = [&](int g, int64_t t, Pl<NP> x) -> Pl<NP> {
+    auto stage = [&](int g, int32_t t, Pl<NP> x) -> Pl<NP> {
         x = stage_step<RULE>(st[g], x, a.birth, a.survive);
         if constexpr (kBirths) {
-            const int64_t r = sg.glob0 + row_first + t - (g + 1);  // field row
-            const bool rok = (r >= 0) && (r < sg.field_h);
+            const int32_t r = t - (g + 1);  // field row, relative to glob0 + row_first
+            const bool rok = (r >= f_lo) && (r < f_hi);
 #pragma unroll
             for (int k = 0; k < NP; ++k) x.v[k] = rok ? (x.v[k] & cm.v[k]) : 0u;
         }
         return x;
     };
-    auto store = [&](int64_t t, const Pl<NP>& x) {
+    auto store = [&](int32_t t, const Pl<NP>& x) {
         if (t >= 2 * K && t < T && st_lane)
-            *reinterpret_cast<Grp<NP>*>(outp + (t - 2 * K) * a.stride) = words_of(x);
+            *reinterpret_cast<Grp<NP>*>(out_rows + (int64_t)(t - 2 * K) * row_bytes + voff) =
+                words_of(x);
     };
 
     // One block of kPrefetch steps from step t0.  GUARD (warm-up blocks): stage g
@@ -399,14 +425,13 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     // saves K*(K-1) of the 2K*K warm-up stage-steps.  In the warm-up blocks of a
     // hand-off kernel, stage g's outputs at steps 2g+2 and 2g+3 (its first two rows,
     // generation g+1) are also stored as side rows 2g and 2g+1 for the block above.
-    auto block = [&](int64_t t0, auto guard) {
+    auto block = [&](int32_t t0, auto guard) {
         constexpr bool kGuard = decltype(guard)::value;
         Pl<NP> x[kPrefetch];
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
             x[p] = ingest(t0 + p, ring[p]);
-            ring[p] = load_grp<NP>(pf);
-            pf += pstride;
+            ring[p] = load_step(t0 + kPrefetch + p);
         }
         // Code placement (steady-state blocks).  gfx950 issues this kernel's
         // instruction mix (DPP move, v_alignbit, v_bitop3 chains; all 8-byte
@@ -419,7 +444,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         // parity is per kernel: loop_place.h, generated by tools/loop_align.py.
         if constexpr (!kGuard) {
             __builtin_amdgcn_sched_barrier(0);
-            place_block<life_loop_pad(K, RULE, NP, HAND) != 0, NP, kPrefetch>(x);
+            place_block<life_loop_pad(K, RULE, NP, HAND, TOFF) != 0, NP, kPrefetch>(x);
             __builtin_amdgcn_sched_barrier(0);
         }
         // stage g of step p only needs stage g-1 of step p and stage g of step
@@ -434,7 +459,9 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
                     x[p] = stage(g, t0 + p, x[p]);
                     if constexpr (HAND && kGuard) {
                         if (g <= K - 2 && (t0 + p == 2 * g + 2 || t0 + p == 2 * g + 3))
-                            store_side<NP>(my_side + (int64_t)(t0 + p - 2) * 64 * G, x[p]);
+                            store_side<NP>(reinterpret_cast<uint64_t*>(
+                                               my_side + (int64_t)(t0 + p - 2) * kSideRowBytes + voff),
+                                           x[p]);
                     }
                 }
             }
@@ -459,11 +486,13 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         }
     }
 
-    // Steady state.  A consumer's last main block (t0 + kPrefetch == R + 2, the
-    // planner keeps R + 2 a multiple of kPrefetch) refills the ring with the
-    // block below's side rows: wait for its flag first.
-    for (int64_t t0 = kWarm; t0 < t_main; t0 += kPrefetch) {
-        if (HAND && consumer && t0 + kPrefetch == t_main) {
+    // Steady state: whole blocks of input steps.  A consumer stops TOFF steps
+    // before t_side; its last whole block's refill is the first to reach t_side
+    // (the planner keeps R + 2 >= warm-up + one block + TOFF), so that block
+    // waits for the flag of the block below first.
+    int32_t t0 = kWarm;
+    for (; consumer ? t0 + kPrefetch + TOFF <= t_side : t0 < T; t0 += kPrefetch) {
+        if (HAND && consumer && t0 + 2 * kPrefetch > t_side) {
             const uint32_t* f = a.flags + (unit - a.strips);
             uint32_t v = 0;
             for (int it = 0; it < kPollLimit; ++it) {
@@ -480,27 +509,46 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
             asm volatile("" ::: "memory");
-            pf = a.side + (unit - a.strips) * a.side_slot + lane * G;
-            pstride = 64 * G;
         }
         block(t0, std::false_type{});
     }
 
     if constexpr (HAND) {
         if (consumer) {
-            // Tail: steps R+2+tau, tau = 0 .. 2K-3.  Side row tau (generation
+            // The planner keeps t_side - warm-up = TOFF (mod kPrefetch): TOFF more
+            // input steps, then the ring holds the tail's first rows after a
+            // compile-time shift by TOFF slots.
+            if constexpr (TOFF > 0) {
+                Pl<NP> x[TOFF];
+#pragma unroll
+                for (int p = 0; p < TOFF; ++p) x[p] = ingest(t0 + p, ring[p]);
+#pragma unroll
+                for (int p = 0; p + TOFF < kPrefetch; ++p) ring[p] = ring[p + TOFF];
+#pragma unroll
+                for (int p = 0; p < TOFF; ++p)
+                    ring[kPrefetch - TOFF + p] = load_step(t0 + kPrefetch + p);
+#pragma unroll
+                for (int d = 0; d < K + TOFF - 1; ++d) {
+#pragma unroll
+                    for (int p = 0; p < TOFF; ++p) {
+                        const int g = d - p;
+                        if (g >= 0 && g < K) x[p] = stage(g, t0 + p, x[p]);
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < TOFF; ++p) store(t0 + p, x[p]);
+            }
+            // Tail: steps t_side + tau, tau = 0 .. 2K-3.  Side row tau (generation
             // tau/2 + 1) enters at stage s0 = tau/2 + 1 in place of stage s0-1's
             // output; stages below s0 are done (their rows are the block below's).
-            const int64_t tb = t_main;
+            const int32_t tb = t_side;
             auto tail = [&](int tau0) {  // tau0: a constant once the loop below is unrolled
                 Pl<NP> x[kPrefetch];
 #pragma unroll
                 for (int p = 0; p < kPrefetch; ++p) {
-                    x[p] = planes_of(ring[p]);
-                    if (tau0 + kPrefetch + p < kSideRows) {
-                        ring[p] = load_grp<NP>(pf);
-                        pf += pstride;
-                    }
+                    x[p] = ingest(tb + tau0 + p, ring[p]);
+                    if (tau0 + kPrefetch + p < kSideRows)
+                        ring[p] = load_step(tb + tau0 + kPrefetch + p);
                 }
 #pragma unroll
                 for (int d = 0; d < K + kPrefetch - 1; ++d) {
@@ -523,26 +571,26 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 
 }  // namespace
 
-template <int K, int NP, bool HAND>
+template <int K, int NP, bool HAND, int TOFF>
 hipError_t launch_kernel(const StepArgs& a, RuleKind rule, hipStream_t s)
 {
     const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
     const dim3 block(64 * kWavesPerBlock);
     switch (rule) {
     case RULE_REF:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, NP, HAND>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, NP, HAND, TOFF>), grid, block, 0, s, a);
         break;
     case RULE_CONWAY:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, NP, HAND>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, NP, HAND, TOFF>), grid, block, 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, NP, HAND>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, NP, HAND, TOFF>), grid, block, 0, s, a);
         break;
     }
     return hipGetLastError();
 }
 
-template <int K, int NP, bool HAND>
+template <int K, int NP, bool HAND, int TOFF>
 int occupancy_kernel(RuleKind rule)
 {
     int blocks = 0;
@@ -550,36 +598,45 @@ int occupancy_kernel(RuleKind rule)
     const int threads = 64 * kWavesPerBlock;
     if (rule == RULE_REF)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_REF, NP, HAND>, threads, 0);
+            &blocks, life_tb_kernel<K, RULE_REF, NP, HAND, TOFF>, threads, 0);
     else if (rule == RULE_CONWAY)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_CONWAY, NP, HAND>, threads, 0);
+            &blocks, life_tb_kernel<K, RULE_CONWAY, NP, HAND, TOFF>, threads, 0);
     else
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, life_tb_kernel<K, RULE_GENERIC, NP, HAND>, threads, 0);
+            &blocks, life_tb_kernel<K, RULE_GENERIC, NP, HAND, TOFF>, threads, 0);
     return e == hipSuccess ? blocks : 0;
 }
 
 // 2-plane lane groups at every depth; 4-plane ones (dev build) up to depth 16,
 // where 5 planes x 4 x K state words still fit the register file.  Hand-off
-// kernels from kHandoffMinDepth on.
+// kernels from kHandoffMinDepth on, with tail offsets 0 and kPrefetch/2
+// (handoff_toff in life_internal.h).
 constexpr bool depth_has_planes(int K, int NP) { return NP == 2 || (kDevKernels && NP == 4 && K <= 16); }
+
+template <int K, int NP>
+hipError_t launch_planes(const StepArgs& a, RuleKind rule, bool hand, hipStream_t s)
+{
+    if constexpr (K >= kHandoffMinDepth) {
+        if (hand) {
+            constexpr int half = kPfOf<NP, K>() / 2;
+            if (a.tail_off == 0) return launch_kernel<K, NP, true, 0>(a, rule, s);
+            if (a.tail_off == half) return launch_kernel<K, NP, true, half>(a, rule, s);
+            return hipErrorInvalidValue;
+        }
+    }
+    return launch_kernel<K, NP, false, 0>(a, rule, s);
+}
 
 template <int K>
 hipError_t launch_depth(const StepArgs& a, RuleKind rule, int planes, bool hand, hipStream_t s)
 {
     if (hand && K < kHandoffMinDepth) return hipErrorInvalidValue;
     if (planes == 4) {
-        if constexpr (depth_has_planes(K, 4)) {
-            if constexpr (K >= kHandoffMinDepth)
-                if (hand) return launch_kernel<K, 4, true>(a, rule, s);
-            return launch_kernel<K, 4, false>(a, rule, s);
-        }
+        if constexpr (depth_has_planes(K, 4)) return launch_planes<K, 4>(a, rule, hand, s);
         return hipErrorInvalidValue;
     }
-    if constexpr (K >= kHandoffMinDepth)
-        if (hand) return launch_kernel<K, 2, true>(a, rule, s);
-    return launch_kernel<K, 2, false>(a, rule, s);
+    return launch_planes<K, 2>(a, rule, hand, s);
 }
 
 template <int K>
@@ -589,18 +646,28 @@ int occupancy_depth(RuleKind rule, int planes, bool hand)
     if (planes == 4) {
         if constexpr (depth_has_planes(K, 4)) {
             if constexpr (K >= kHandoffMinDepth)
-                if (hand) return occupancy_kernel<K, 4, true>(rule);
-            return occupancy_kernel<K, 4, false>(rule);
+                if (hand) return occupancy_kernel<K, 4, true, 0>(rule);
+            return occupancy_kernel<K, 4, false, 0>(rule);
         }
         return 0;
     }
     if constexpr (K >= kHandoffMinDepth)
-        if (hand) return occupancy_kernel<K, 2, true>(rule);
-    return occupancy_kernel<K, 2, false>(rule);
+        if (hand) return occupancy_kernel<K, 2, true, 0>(rule);
+    return occupancy_kernel<K, 2, false, 0>(rule);
 }
 
+// Instantiation per depth.  A depth's hand-off kernels can be split into their
+// own translation units (GOL_EXTERN_HAND in the depth's unit, GOL_INSTANTIATE_HAND
+// in the others) to keep the build parallel.
 #define GOL_INSTANTIATE_DEPTH(K)                                                              \
     template hipError_t launch_depth<K>(const StepArgs&, RuleKind, int, bool, hipStream_t);   \
     template int occupancy_depth<K>(RuleKind, int, bool);
+#define GOL_INSTANTIATE_HAND(K, T)                                                            \
+    template hipError_t launch_kernel<K, 2, true, T>(const StepArgs&, RuleKind, hipStream_t); \
+    template int occupancy_kernel<K, 2, true, T>(RuleKind);
+#define GOL_EXTERN_HAND(K, T)                                                                 \
+    extern template hipError_t launch_kernel<K, 2, true, T>(const StepArgs&, RuleKind,        \
+                                                            hipStream_t);                     \
+    extern template int occupancy_kernel<K, 2, true, T>(RuleKind);
 
 }  // namespace gol

@@ -8,7 +8,7 @@ identical instructions and register allocation differ only in that placement
 (profiles/r01/loop_alignment_ab.jsonl, tools/valu_rate.hip "mix_at_*").
 life_kernels.hip aligns the compute of each steady-state block to 8 bytes and
 adds a 4-byte s_nop when csrc/loop_place.h says so.  This tool reads the built
-libgol.so, reports per life_tb_kernel<K, RULE, NP, HAND> the share of the main
+libgol.so, reports per life_tb_kernel<K, RULE, NP, HAND, TOFF> the share of the main
 loop's 8-byte instructions at the wanted parity (4 mod 8 when the kernel's
 registers admit 2+ waves per SIMD, from the code object's .vgpr_count), and
 with --update flips the pad of misplaced kernels in loop_place.h (rebuild
@@ -27,8 +27,8 @@ import tempfile
 LLVM = "/opt/rocm/lib/llvm/bin"
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = os.path.join(HERE, "..", "mpi-game-of-life_amd", "csrc", "loop_place.h")
-KRE = re.compile(r"^[0-9a-f]+ <_ZN3gol12_GLOBAL__N_114life_tb_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)EEEvNS_8StepArgsE>:")
-NRE = re.compile(r"life_tb_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)EEEvNS_8StepArgsE")
+KRE = re.compile(r"^[0-9a-f]+ <_ZN3gol12_GLOBAL__N_114life_tb_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)EEEvNS_8StepArgsE>:")
+NRE = re.compile(r"life_tb_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)EEEvNS_8StepArgsE")
 
 
 def disassemble_one(obj):
@@ -60,7 +60,7 @@ def disassemble(so):
 
 
 def vgpr_counts(notes):
-    """{(K, RULE, NP, HAND): .vgpr_count} of the stencil kernels, from the code
+    """{(K, RULE, NP, HAND, TOFF): .vgpr_count} of the stencil kernels, from the code
     object metadata (gfx950: one unified register file, 512 per SIMD lane)."""
     out, name, vg = {}, None, None
     for l in notes.split("\n") + ["- end"]:
@@ -98,40 +98,46 @@ def main_loop_fraction(body):
             cands.append((lo, hi, eight))
     if not cands:
         return None, 0
-    lo, hi, eight = max(cands, key=lambda c: (c[0], -c[1]))  # last loop, innermost
+    # the steady-state loop: of the innermost candidate loops, the one with the most
+    # compute (the control flow may wrap bigger loops around it)
+    inner = [c for c in cands
+             if not any(d is not c and c[0] <= d[0] and d[1] <= c[1] for d in cands)]
+    lo, hi, eight = max(inner, key=lambda c: len(c[2]))
     return sum(1 for a in eight if a % 8 == 4) / len(eight), len(eight)
 
 
 def current_pads():
     pads = set()
     if os.path.exists(HEADER):
-        for m in re.finditer(r"\{(\d+), (\d+), (\d+), (\d+)\}", open(HEADER).read()):
+        for m in re.finditer(r"\{(\d+), (\d+), (\d+), (\d+), (\d+)\}", open(HEADER).read()):
             if m.group(1) != "0":
                 pads.add(tuple(int(x) for x in m.groups()))
     return pads
 
 
 def write_header(pads):
-    rows = "".join(f"    {{{k}, {r}, {n}, {h}}},\n" for k, r, n, h in sorted(pads))
+    rows = "".join(f"    {{{k}, {r}, {n}, {h}, {t}}},\n" for k, r, n, h, t in sorted(pads))
     open(HEADER, "w").write(f"""// loop_place.h -- GENERATED by tools/loop_align.py --update from the built
-// libgol.so; do not edit by hand.  life_loop_pad(K, RULE, NP, HAND) = 1 adds a
-// 4-byte s_nop after the 8-byte alignment before the compute of each
-// steady-state block of life_tb_kernel<K, RULE, NP, HAND> (see life_stencil.h).
+// libgol.so; do not edit by hand.  life_loop_pad(K, RULE, NP, HAND, TOFF) = 1
+// adds a 4-byte s_nop after the 8-byte alignment before the compute of each
+// steady-state block of life_tb_kernel<K, RULE, NP, HAND, TOFF> (see
+// life_stencil.h).
 #pragma once
 
 namespace gol {{
 
 struct LoopPad {{
-    int K, rule, np, hand;
+    int K, rule, np, hand, toff;
 }};
 constexpr LoopPad kLoopPads[] = {{
-{rows}    {{0, 0, 0, 0}}  // end
+{rows}    {{0, 0, 0, 0, 0}}  // end
 }};
 
-constexpr int life_loop_pad(int K, int RULE, int NP, bool HAND)
+constexpr int life_loop_pad(int K, int RULE, int NP, bool HAND, int TOFF)
 {{
     for (const LoopPad& p : kLoopPads)
-        if (p.K == K && p.rule == RULE && p.np == NP && p.hand == (HAND ? 1 : 0)) return 1;
+        if (p.K == K && p.rule == RULE && p.np == NP && p.hand == (HAND ? 1 : 0) && p.toff == TOFF)
+            return 1;
     return 0;
 }}
 
@@ -163,7 +169,7 @@ def main():
         good = frac if want4 else 1.0 - frac
         hot = key[1] in (0, 1) and key[0] >= 8
         ok = good >= 0.9
-        print(f"life_tb_kernel<{key[0]:2d}, {key[1]}, {key[2]}, {bool(key[3])}> ({vgprs.get(key, '?')} regs): "
+        print(f"life_tb_kernel<{key[0]:2d}, {key[1]}, {key[2]}, {bool(key[3])}, {key[4]}> ({vgprs.get(key, '?')} regs): "
               f"{n:5d} 8-byte instrs, "
               f"{100 * good:3.0f}% at {'4' if want4 else '0'} mod 8, pad {int(key in pads)}"
               f"{'' if ok else '  <- misplaced'}")

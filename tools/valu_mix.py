@@ -45,11 +45,16 @@ def loop_body(body):
         m = re.search(r"s_c?branch\w* .*\+0x([0-9a-f]+)>", l)
         if m and int(m.group(1), 16) + base < a:
             loops.append((int(m.group(1), 16) + base, a))
-    cands = [(lo, hi) for lo, hi in loops
-             if sum(1 for a, sz, _, _ in ins if lo <= a <= hi and sz == 8) >= 32]
+    cands = [(lo, hi, sum(1 for a, sz, _, _ in ins if lo <= a <= hi and sz == 8))
+             for lo, hi in loops]
+    cands = [c for c in cands if c[2] >= 32]
     if not cands:
         return None
-    lo, hi = max(cands, key=lambda c: (c[0], -c[1]))
+    # the steady-state loop: of the innermost candidate loops, the one with the most
+    # compute (the control flow may wrap bigger loops around it)
+    inner = [c for c in cands
+             if not any(d is not c and c[0] <= d[0] and d[1] <= c[1] for d in cands)]
+    lo, hi, _ = max(inner, key=lambda c: c[2])
     return [(mn, l) for a, _, mn, l in ins if lo <= a <= hi]
 
 
@@ -62,7 +67,7 @@ def main():
         m = la.KRE.match(l)
         if not m:
             continue
-        K, rule, np_, hand = (int(x) for x in m.groups())
+        K, rule, np_, hand, toff = (int(x) for x in m.groups())
         end = next(j for j in range(i + 1, len(lines)) if not lines[j].strip())
         body = loop_body(lines[i:end])
         if body is None:
@@ -80,14 +85,14 @@ def main():
         per = {k: round(v / steps, 3) for k, v in cnt.items()}
         slots = (cnt.get("valu_full", 0) + 2 * cnt.get("valu_half", 0)) / steps
         stage_slots = (bitop3 + 2 * (dpp + align)) / steps
-        rec = {"K": K, "rule": rule, "np": np_, "hand": bool(hand), "vgprs": vg.get((K, rule, np_, hand)),
+        rec = {"K": K, "rule": rule, "np": np_, "hand": bool(hand), "toff": toff, "vgprs": vg.get((K, rule, np_, hand, toff)),
                "loop_instrs": len(body), "stage_steps_per_iter": steps,
                "per_stage_step": per, "v_bitop3": round(bitop3 / steps, 3),
                "dpp": round(dpp / steps, 3), "v_alignbit": round(align / steps, 3),
                "valu_slots_per_stage_step": round(slots, 3),
                "stage_logic_slots_per_stage_step": round(stage_slots, 3)}
         recs.append(rec)
-        print(f"<{K:2d},{rule},{np_},{int(hand)}> per stage-step: bitop3 {rec['v_bitop3']:5.2f} "
+        print(f"<{K:2d},{rule},{np_},{int(hand)},{toff}> per stage-step: bitop3 {rec['v_bitop3']:5.2f} "
               f"dpp {rec['dpp']:4.2f} alignbit {rec['v_alignbit']:4.2f} | all VALU slots "
               f"{slots:5.2f} (stage logic {stage_slots:5.2f}) | {per}")
     if out:
