@@ -289,8 +289,11 @@ bool handoff_fits(int64_t R, int d, int planes) { return gol::handoff_toff(R, d,
 // loaded SIMD: n = ceil(units / SIMDs) wavefronts run in rounds of `occ`
 // resident ones, and a partial round of m wavefronts still costs max(2, m) issue
 // slots per instruction (one wavefront alone issues at half the SIMD's VALU rate).
-// A wavefront's work in rows of K stage-steps: classic blocks R + K + 1 (+ c0
-// fixed), hand-off blocks R + 2 (+ c0 + the hand-off's own cost).  Measured
+// A wavefront's time in rows of K stage-steps: classic blocks R + K + 1 (+ c0
+// fixed); hand-off blocks skip the K - 1 rows of vertical halo but their steady
+// loop runs ~4% slower per row (bigger code, side-row refills):
+// 1.04 R + 8, fitted to the in-process A/B of profiles/r02/ab_handoff_*.jsonl
+// (8448 rows: hand-off 5% faster; 33024 / 65536 rows: classic 1-3% faster).  Measured
 // (profiles/r01/sweep_rows_per_wave*.jsonl): keeping fewer than `occ`
 // wavefronts per SIMD all launch long is 5-10% slower than the model says, so R
 // is restricted to n >= occ whenever the field is large enough.  Narrower strips
@@ -306,8 +309,7 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
                            int occ_classic, int occ_hand, int simds, int force_rpw,
                            int force_shift, uint32_t handoff)
 {
-    const int64_t c0 = 3;      // per-wavefront fixed cost, in rows
-    const int64_t c_hand = 2;  // side-row stores, flag wait, shorter tail ILP
+    const int64_t c0 = 3;  // per-wavefront fixed cost, in rows
     int64_t maxrows = 1;
     for (const auto& s : segs) maxrows = std::max<int64_t>(maxrows, s.out_hi - s.out_lo);
     // best [hand][filled]: filled = at least `occ` wavefronts per SIMD
@@ -336,7 +338,7 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
                 const int64_t full = n / occ, rem = n % occ;
                 const double slots =
                     (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
-                const double rows = hand ? (double)(R + 2 + c0 + c_hand) : (double)(R + K + 1 + c0);
+                const double rows = hand ? 1.04 * (double)R + 8.0 : (double)(R + K + 1 + c0);
                 const double cost = slots * rows;
                 const int filled = n >= occ ? 1 : 0;
                 if (cost < best[hand][filled] * 0.999) {

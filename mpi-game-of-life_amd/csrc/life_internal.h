@@ -95,15 +95,16 @@ constexpr int warm_steps_of(int K, int planes)
 }
 // Hand-off kernels exist for tail offsets 0 and prefetch/2: a consumer block of R
 // rows streams R + 2 input steps after the warm-up, i.e. (R + 2 - warm) mod
-// prefetch must be one of them, and at least one whole block must precede the
-// tail.  Returns the offset, or -1 if R does not fit.
+// prefetch must be one of them, and at least two whole steady blocks must precede
+// the tail (the flag wait sits at the end of the first of them).  Returns the
+// offset, or -1 if R does not fit.
 constexpr int handoff_toff(int64_t R, int K, int planes)
 {
     const int pf = prefetch_of(K, planes), warm = warm_steps_of(K, planes);
-    if (K < kHandoffMinDepth || R + 2 < warm + pf) return -1;
+    if (K < kHandoffMinDepth || R + 2 < warm + 2 * pf) return -1;
     const int off = (int)((R + 2 - warm) % pf);
     if (off != 0 && off != pf / 2) return -1;
-    return R + 2 - off >= warm + pf ? off : -1;
+    return R + 2 - off >= warm + 2 * pf ? off : -1;
 }
 
 // Launch `depth` fused generations (depth in kDepthList) on lane groups of

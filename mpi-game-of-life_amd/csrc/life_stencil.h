@@ -300,6 +300,13 @@ __device__ __forceinline__ void place_block(Pl<NP> (&x)[PF])
 // so that the launch always drains.
 constexpr int kPollLimit = 1 << 16;
 
+// Dev timing experiments only (tools/exp_build.sh; results are NOT valid): bit 0
+// skips the consumer's wait, bit 1 the producer's drain + flag, bit 2 the
+// side-row stores, bit 3 the consumer's tail.
+#ifndef GOL_EXP
+#define GOL_EXP 0
+#endif
+
 template <int K, int RULE, int NP, bool HAND, int TOFF>
 __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
 {
@@ -307,6 +314,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     constexpr int G = NP / 2;  // words per lane group
     constexpr int kPrefetch = kPfOf<NP, K>();
     constexpr int kSideRows = 2 * (K - 1);  // hand-off rows per block: 2 per generation 1..K-1
+    constexpr int kWarmSteps = (2 * K + kPrefetch - 1) / kPrefetch * kPrefetch;  // unrolled warm-up
     static_assert(K + 2 * kPrefetch <= kGuardRows, "streaming loads must stay in the guard rows");
     static_assert(!HAND || K >= kHandoffMinDepth, "hand-off kernels start at kHandoffMinDepth");
     static_assert(TOFF >= 0 && TOFF < kPrefetch && (HAND || TOFF == 0), "tail offset");
@@ -339,11 +347,14 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         cm.v[k] = qin ? ((q == a.ng - 1) ? (uint32_t)(a.lastmask[k / 2] >> (32 * (k & 1))) : ~0u)
                       : 0u;
     // lanes outside the field read the strip's first group (any word of the row
-    // will do; masked to 0); qc - qbase is in [0, 64) on every lane, which is how
-    // the lanes index a 64-entry side row
+    // will do; masked to 0)
     const int64_t qc = qin ? q : qbase + 1;
-    // Every access = a uniform row base (SGPRs) + this per-lane byte offset.
+    // Every access = a uniform row base (SGPRs) + a per-lane byte offset: the
+    // lane's group in field rows, the lane itself in side rows (halo lanes and
+    // lanes outside the field share groups with other lanes, so side rows, which
+    // every lane stores, are indexed by lane)
     const uint32_t voff = (uint32_t)(qc * G * 8);
+    const uint32_t voff_side = (uint32_t)(lane * G * 8);
 
     const int64_t rb = sg.out_lo + blk * a.rows_per_wave;
     const int64_t re = min(rb + a.rows_per_wave, sg.out_hi);
@@ -362,11 +373,9 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     char* out_rows = reinterpret_cast<char*>(a.out + (sg.base_row + rb) * a.stride);
     const int64_t row_bytes = a.stride * 8;
     constexpr int64_t kSideRowBytes = 64 * G * 8;
-    // slot bases shifted by qbase so that slot entry (qc - qbase) is at base + voff
-    char* my_side = HAND ? reinterpret_cast<char*>(a.side + unit * a.side_slot - qbase * G) : nullptr;
+    char* my_side = HAND ? reinterpret_cast<char*>(a.side + unit * a.side_slot) : nullptr;
     const char* dn_side =
-        HAND ? reinterpret_cast<const char*>(a.side + (unit - a.strips) * a.side_slot - qbase * G)
-             : nullptr;
+        HAND ? reinterpret_cast<const char*>(a.side + (unit - a.strips) * a.side_slot) : nullptr;
     const bool st_lane = qin && lin >= 1 && lin <= L - 2;
 
     // field-row validity of the row of step t (dead border) and buffer-row validity:
@@ -385,9 +394,12 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     // the row streamed at step s: input row row_first + s, or for a consumer from
     // step t_side on the block below's side row s - t_side (uniform select)
     auto load_step = [&](int32_t s) -> Grp<NP> {
-        const char* base = s < t_side ? in_rows + (int64_t)s * row_bytes
-                                      : dn_side + (int64_t)(s - t_side) * kSideRowBytes;
-        return load_grp<NP>(reinterpret_cast<const uint64_t*>(base + voff));
+        if constexpr (!HAND)
+            return load_grp<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
+        const bool in = s < t_side;
+        const char* base = in ? in_rows + (int64_t)s * row_bytes
+                              : dn_side + (int64_t)(s - t_side) * kSideRowBytes;
+        return load_grp<NP>(reinterpret_cast<const uint64_t*>(base + (in ? voff : voff_side)));
     };
     Grp<NP> ring[kPrefetch];
 #pragma unroll
@@ -396,7 +408,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     // row of step t: an input row is dead outside the field / buffer; a side row
     // comes as the block below computed it; columns >= w masked
     auto ingest = [&](int32_t t, const Grp<NP>& xv) -> Pl<NP> {
-        const bool ok = t >= t_side || ((t >= t_lo) && (t < t_hi));
+        const bool ok = (HAND && t >= t_side) || ((t >= t_lo) && (t < t_hi));
         Pl<NP> x = planes_of(xv);
 #pragma unroll
         for (int k = 0; k < NP; ++k) x.v[k] = ok ? (x.v[k] & cm.v[k]) : 0u;
@@ -417,6 +429,43 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         if (t >= 2 * K && t < T && st_lane)
             *reinterpret_cast<Grp<NP>*>(out_rows + (int64_t)(t - 2 * K) * row_bytes + voff) =
                 words_of(x);
+    };
+
+    // Hand-off signalling (HAND kernels), done in steady blocks after the compute:
+    //  * a producer (every block but the top one) raises its flag after its first
+    //    steady block -- its side rows were all stored in the warm-up blocks, and
+    //    s_waitcnt vmcnt(0) there finds them long complete;
+    //  * a consumer waits for the flag of the block below at the end of the block
+    //    before the one whose refill first fetches side rows (the planner keeps
+    //    R + 2 >= warm-up + 2 blocks + tail offset, handoff_toff).
+    auto signal = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            __hip_atomic_store(a.flags + unit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto wait_below = [&]() {
+        const uint32_t* f = a.flags + (unit - a.strips);
+        uint32_t v = 0;
+        for (int it = 0; it < ((GOL_EXP & 1) ? 0 : kPollLimit); ++it) {
+            v = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT));
+            if (v) break;
+            __builtin_amdgcn_s_sleep(8);
+        }
+        if (lane == 0) {
+            if (!v && !(GOL_EXP & 1))
+                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // flags are all 0 between launches: reset the producer's
+            __hip_atomic_store(const_cast<uint32_t*>(f), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("" ::: "memory");
+    };
+    auto sync_point = [&](int32_t t0) {
+        if (producer && t0 == kWarmSteps && !(GOL_EXP & 2)) signal();
+        if (consumer && t0 + 3 * kPrefetch + TOFF > t_side && t0 + 2 * kPrefetch + TOFF <= t_side)
+            wait_below();
     };
 
     // One block of kPrefetch steps from step t0.  GUARD (warm-up blocks): stage g
@@ -457,63 +506,43 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
                 const int g = d - p;
                 if (g >= 0 && g < K && (!kGuard || t0 + p >= 2 * g)) {
                     x[p] = stage(g, t0 + p, x[p]);
-                    if constexpr (HAND && kGuard) {
+                    if constexpr (HAND && kGuard && !(GOL_EXP & 4)) {
                         if (g <= K - 2 && (t0 + p == 2 * g + 2 || t0 + p == 2 * g + 3))
                             store_side<NP>(reinterpret_cast<uint64_t*>(
-                                               my_side + (int64_t)(t0 + p - 2) * kSideRowBytes + voff),
+                                               my_side + (int64_t)(t0 + p - 2) * kSideRowBytes +
+                                               voff_side),
                                            x[p]);
                     }
                 }
             }
         }
-        if constexpr (!kGuard) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!kGuard) {
+            __builtin_amdgcn_sched_barrier(0);
+            // hand-off signalling between this block's compute and its stores: the
+            // memory operations still outstanding here (this block's refill, the
+            // previous block's stores) were issued a whole block of compute ago
+            if constexpr (HAND) sync_point(t0);
+        }
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) store(t0 + p, x[p]);
     };
 
     // Warm-up blocks, unrolled (compile-time guards).
-    constexpr int kWarm = (2 * K + kPrefetch - 1) / kPrefetch * kPrefetch;
+    constexpr int kWarm = kWarmSteps;
     static_assert(!HAND || kWarm >= 2 * K, "side rows are all stored in the warm-up blocks");
 #pragma unroll
     for (int t0 = 0; t0 < kWarm; t0 += kPrefetch) block(t0, std::true_type{});
 
-    if constexpr (HAND) {
-        // side rows 0..2K-3 stored: make them visible, then raise the flag
-        if (producer) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_store(a.flags + unit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-
     // Steady state: whole blocks of input steps.  A consumer stops TOFF steps
-    // before t_side; its last whole block's refill is the first to reach t_side
-    // (the planner keeps R + 2 >= warm-up + one block + TOFF), so that block
-    // waits for the flag of the block below first.
+    // before t_side; its last whole block's refill is the first to reach t_side.
     int32_t t0 = kWarm;
-    for (; consumer ? t0 + kPrefetch + TOFF <= t_side : t0 < T; t0 += kPrefetch) {
-        if (HAND && consumer && t0 + 2 * kPrefetch > t_side) {
-            const uint32_t* f = a.flags + (unit - a.strips);
-            uint32_t v = 0;
-            for (int it = 0; it < kPollLimit; ++it) {
-                v = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT));
-                if (v) break;
-                __builtin_amdgcn_s_sleep(8);
-            }
-            if (lane == 0) {
-                if (!v) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // flags are all 0 between launches: reset the producer's
-                __hip_atomic_store(const_cast<uint32_t*>(f), 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-            asm volatile("" ::: "memory");
-        }
+    for (; consumer ? t0 + kPrefetch + TOFF <= t_side : t0 < T; t0 += kPrefetch)
         block(t0, std::false_type{});
-    }
+    // a producer whose stream had no steady block (a short last block) signals here
+    if constexpr (HAND)
+        if (producer && T <= kWarm && !(GOL_EXP & 2)) signal();
 
-    if constexpr (HAND) {
+    if constexpr (HAND && !(GOL_EXP & 8)) {
         if (consumer) {
             // The planner keeps t_side - warm-up = TOFF (mod kPrefetch): TOFF more
             // input steps, then the ring holds the tail's first rows after a

@@ -26,8 +26,8 @@ def test_group_matches_single_field(pkg, oracle, nranks, rule):
                                          (2, 5, 11, 0, 0, 0), (1, 3, 7, 0, 0, 0),
                                          (16, 16, 33, 0, 0, 0), (8, 0, 37, 1, 0, 0),
                                          (16, 24, 50, 1, 0, 0), (16, 0, 70, 0, 32, 0),
-                                         (8, 0, 37, 0, 16, 0), (8, 0, 37, 2, 0, 18),
-                                         (16, 0, 40, 2, 0, 38), (4, 16, 45, 2, 0, 10)):
+                                         (8, 0, 37, 0, 16, 0), (8, 0, 37, 2, 0, 22),
+                                         (16, 0, 40, 2, 0, 46), (4, 16, 45, 2, 0, 14)):
         ref = oracle.bp_run(g, w, gens, R)
         with pkg.Group(h, w, nranks, rule=R, tb_depth=tb, halo_depth=hx, handoff=ho,
                        strip_lanes=lanes, rows_per_wave=rpw) as grp:

@@ -117,20 +117,33 @@ def test_strip_widths(pkg, oracle, lanes, rule):
                     assert (e.store_packed() == ref).all(), f"{h}x{w} depth {depth} gens {gens}"
 
 
-@pytest.mark.parametrize("rpw", [14, 16, 30, 32, 46, 48, 100])
+def handoff_toff(R, K):
+    """life_internal.h handoff_toff (2-plane lane groups): the tail offset of a
+    hand-off launch with R rows per wavefront, or -1 if R does not fit."""
+    pf = 8 if K >= 16 else 4
+    warm = -(-2 * K // pf) * pf
+    if K < 4 or R + 2 < warm + 2 * pf:
+        return -1
+    off = (R + 2 - warm) % pf
+    if off not in (0, pf // 2):
+        return -1
+    return off if R + 2 - off >= warm + 2 * pf else -1
+
+
+@pytest.mark.parametrize("rpw", [14, 16, 22, 24, 30, 31, 32, 46, 48, 100])
 @pytest.mark.parametrize("handoff", [1, 2])
 def test_row_blocking(pkg, oracle, rpw, handoff):
     """Many row blocks per strip (rows_per_wave small): block seams exact, both
-    block closures.  Hand-off needs R + 2 to be a whole number of prefetch blocks
-    (4 steps at depth 8) and at least the 16 warm-up steps + one block: 30 and 46
-    hand over, the others fall back to classic blocks."""
+    block closures.  Hand-off needs R + 2 - warm-up (16 steps at depth 8) to be 0
+    or 2 modulo the 4-step prefetch block and at least 2 blocks: from 22 rows on,
+    even R hand over, the others fall back to classic blocks."""
     h, w = 300, 4100
     g = oracle.bp_random(h, w, 5)
     ref = oracle.bp_run(g, w, 16, oracle.CONWAY)
     for lanes in (64, 32, 16):
         with pkg.Engine(h, w, rule=oracle.CONWAY, device=0, tb_depth=8, rows_per_wave=rpw,
                         handoff=handoff, strip_lanes=lanes) as e:
-            assert e.handoff == (handoff == 2 and (rpw + 2) % 4 == 0 and rpw + 2 >= 20)
+            assert e.handoff == (handoff == 2 and handoff_toff(rpw, 8) >= 0)
             e.init_random(5)
             e.step(16)
             assert (e.store_packed() == ref).all(), (lanes, rpw)
@@ -144,9 +157,7 @@ def test_handoff_seams(pkg, oracle, depth, rule):
     seams (Conway / HighLife), odd widths, and remainder launches of smaller
     depth in the same call.  Must equal the oracle and the classic blocks."""
     R = rules(oracle)[rule]
-    pf = 8 if depth >= 16 else 4
-    warm = -(-2 * depth // pf) * pf
-    rpw = warm + pf - 2
+    rpw = min(r for r in range(4, 200) if handoff_toff(r, depth) >= 0)
     for h, w in ((5 * rpw + 3, 130), (3 * rpw, 4100), (2 * rpw + 1, 63)):
         g = oracle.bp_random(h, w, h + depth)
         for gens in (depth, 3 * depth + 5):
@@ -160,12 +171,31 @@ def test_handoff_seams(pkg, oracle, depth, rule):
                     assert (e.store_packed() == ref).all(), (h, w, gens, handoff)
 
 
+@pytest.mark.parametrize("depth", [8, 12, 16])
+@pytest.mark.parametrize("toff", [0, 1])
+def test_handoff_tail_offsets(pkg, oracle, depth, toff):
+    """Both hand-off kernels of a depth: R + 2 - warm-up = 0 and = prefetch/2
+    (mod the prefetch block), Conway so the tails' stages do real work."""
+    pf = 8 if depth >= 16 else 4
+    rs = [r for r in range(4, 300) if handoff_toff(r, depth) == toff * pf // 2]
+    for rpw in rs[:2]:
+        h, w = 4 * rpw + 7, 2000
+        g = oracle.bp_random(h, w, rpw + depth)
+        ref = oracle.bp_run(g, w, 2 * depth + 3, oracle.CONWAY)
+        with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, tb_depth=depth, rows_per_wave=rpw,
+                        handoff=2, streams=1) as e:
+            assert e.handoff
+            e.load_packed(g)
+            e.step(2 * depth + 3)
+            assert (e.store_packed() == ref).all(), rpw
+
+
 def test_handoff_repeated_launches_and_graphs(pkg, oracle):
     """Hand-off flags are reset by every consumer, so back-to-back launches, graph
     replays and alternating call sizes (different remainder depths) stay exact."""
     h, w = 1000, 3000
     g = oracle.bp_random(h, w, 77)
-    with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, tb_depth=16, rows_per_wave=38,
+    with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, tb_depth=16, rows_per_wave=46,
                     handoff=2, streams=1) as e:
         assert e.handoff
         e.load_packed(g)
