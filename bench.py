@@ -13,12 +13,28 @@ RCCL halo exchanges (strong scaling: total work fixed).
 
 Timed region: W untimed steps, then barrier + device sync, K steps, device sync
 + barrier; max over ranks.  The field is resident in HBM throughout.  Rank 0
-prints one JSON line.  `roofline` prices the stencil kernel at SURVEY §8(d)'s
-0.25 algorithmic bytes per cell-generation (1 bit read + 1 bit written) against
-8 TB/s, using HIP events recorded around every launch on the engine's stream;
+prints one JSON line.
+
+`roofline` names the bound that binds.  The stencil kernel is temporally blocked
+(K = 16 generations per launch) and VALU-issue bound, not HBM bound (DESIGN.md
+§4), so:
+  * bound "valu": achieved = the stage logic's VALU issue slots per second of
+    the timed launches -- cell-generations per launch / 4096 cells per
+    wave-instruction x slots per lane group and generation (24 for B/S2: 16
+    v_bitop3 + 2 DPP moves and 2 v_alignbit at two slots each; static count of
+    the steady-state loop, profiles/r02/valu_mix.json) / the mean HIP-event
+    launch time x concurrent streams; peak = 1024 SIMDs x the best measured
+    full-rate VALU issue rate (profiles/r01/valu_rate.json); frac <= 1;
+  * valu.issue_frac: ALL VALU instructions per launch (rocprofv3 SQ_INSTS_VALU
+    of this configuration, committed in profiles/r02/counters.json: warm-up,
+    masks and halo work included) at the same peak;
+  * hbm_equiv_frac: SURVEY §8(d)'s 0.25 B per cell-generation x GCUPS / 8 TB/s
+    (> 1 is what temporal blocking buys); hbm_measured_frac: the measured HBM
+    bytes per launch (FETCH_SIZE/WRITE_SIZE, calibrated; `traffic`) x launches/s.
 `cpu_baseline` times the oracle's scalar port of the reference algorithm
-(oracle/gol_oracle.c, int per cell, per-cell neighbour loop) on a bounded
-sample on this host's cores.
+(oracle/gol_oracle.c: int per cell, per-cell neighbour loop, Parallel_Life_MPI.cpp
+:16-54) on this host's allowed cores, on the benchmark's own field; the reference
+binary itself cannot be built here (it includes <windows.h>, :6).
 """
 import argparse
 import json
@@ -34,6 +50,11 @@ import __graft_entry__ as entry  # noqa: E402
 METRIC = "cell updates/sec (GCUPS) at 65536^2, 1/2/4/8 GPUs; % of HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_CELL_GEN = 0.25
+SIMDS = 1024  # 256 CUs x 4
+CELLS_PER_WAVE_INSTR = 64 * 64  # 64 lanes x one 64-column lane group (2 planes)
+# VALU issue slots per lane group and generation of the stage logic (v_bitop3 = 1,
+# DPP move and v_alignbit = 2 each): tools/valu_mix.py, profiles/r02/valu_mix.json
+STAGE_SLOTS = {"ref": 24, "conway": 28}
 
 
 def parse():
@@ -44,54 +65,105 @@ def parse():
     p.add_argument("--size", type=int, default=65536, help="field is size x size")
     p.add_argument("--gens", type=int, default=1000, help="generations per step")
     p.add_argument("--tb-depth", type=int, default=0)
-    p.add_argument("--word-planes", type=int, default=0)
     p.add_argument("--rows-per-wave", type=int, default=0)
     p.add_argument("--halo-depth", type=int, default=0)
+    p.add_argument("--handoff", type=int, default=0)
+    p.add_argument("--streams", type=int, default=0)
     p.add_argument("--rule", default="ref", choices=["ref", "conway"])
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = the allowed CPUs")
     return p.parse_args()
 
 
-def cpu_baseline(threads, w):
-    """Oracle port of the reference algorithm, bounded sample: `threads` stripes of
-    512 rows x w columns (like mpirun -np threads), 16 generations."""
+def load_json(rel):
+    try:
+        return json.load(open(os.path.join(ROOT, rel)))
+    except Exception:
+        return None
+
+
+def valu_peak_rate():
+    """Best measured full-rate VALU issue rate per SIMD (wave-instructions/s)."""
+    r = load_json("profiles/r01/valu_rate.json") or {}
+    return max(r.get("v_bitop3_b32_at_0mod8_2waves", 0.0), r.get("v_xor_b32", 0.0), 9.0e8)
+
+
+def counters_for(cfg):
+    """Per-launch PMC record (SQ_INSTS_VALU, HBM bytes) of this configuration."""
+    rec = load_json("profiles/r02/counters.json") or {}
+    for r in rec.get("records", []):
+        if all(r.get(k) == cfg.get(k) for k in ("size", "rule", "tb_depth", "streams", "n_gpus",
+                                                "rows_per_wave", "handoff")):
+            return r
+    return None
+
+
+def host_info():
+    """CPU model, the CPUs this process may run on, their physical cores, compiler."""
+    import platform
+    import subprocess
+    allowed = sorted(os.sched_getaffinity(0))
+    cores = set()
+    for c in allowed:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            cores.add((open(base + "physical_package_id").read().strip(),
+                       open(base + "core_id").read().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    model = platform.processor()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        cc = subprocess.run(["gcc", "--version"], capture_output=True,
+                            text=True).stdout.split("\n")[0]
+    except Exception:
+        cc = "gcc"
+    return {"cpu_model": model, "cpus_allowed": len(allowed), "physical_cores": len(cores),
+            "compiler": cc + ", -O2 -fPIC (oracle/Makefile)"}
+
+
+def cpu_baseline(w, seed, threads=0):
+    """Oracle port of the reference algorithm (int per cell, per-cell neighbour
+    loop) on the benchmark's own field: `threads` stripes of 256 rows x w columns
+    (rows [0, threads*256) of the splitmix64 field), each evolved alone like one
+    `mpirun -np threads` rank, E = 32 generations of B/S2; GCUPS from
+    T(E) - T(0), so building the field is not counted."""
+    info = host_info()
+    if not threads:
+        threads = info["cpus_allowed"]
+        omp = os.environ.get("OMP_NUM_THREADS")
+        if omp and omp.isdigit():  # the box's CPU share (set there)
+            threads = min(threads, int(omp))
     orc = entry.load_oracle()
-    rows, gens = 512, 64
+    rows, gens = 256, 32
     t0 = time.perf_counter()
-    orc.ref_baseline(rows, w, 0, threads)
+    orc.ref_baseline(rows, w, 0, threads, seed)
     t_init = time.perf_counter() - t0
     t0 = time.perf_counter()
-    orc.ref_baseline(rows, w, gens, threads)
+    orc.ref_baseline(rows, w, gens, threads, seed)
     t = time.perf_counter() - t0 - t_init
-    cells = threads * rows * w * gens
-    return {
-        "value": round(cells / t / 1e9, 4),
+    gcups = threads * rows * w * gens / t / 1e9
+    rec = {
+        "value": round(gcups, 4),
         "unit": "GCUPS",
         "cores": threads,
         "kind": "port",
-        "sample": f"{threads} stripes x {rows} rows x {w} cols, {gens} gens, int32 per cell, "
-                  f"per-cell countNeighbours loop (Parallel_Life_MPI.cpp:16-54), "
-                  f"{t:.1f} s, init subtracted",
+        "why_port": "the reference binary is unbuildable here: Parallel_Life_MPI.cpp:6 "
+                    "includes <windows.h>",
+        "sample": f"{threads} stripes x {rows} rows x {w} cols of the bench field (splitmix64 "
+                  f"seed {seed}), E = {gens} generations of B/S2 (dense for ~3 generations, "
+                  f"then sparse), T(E) - T(0) = {t:.2f} s",
+        "per_core_mcups": round(gcups * 1e3 / threads, 1),
     }
-
-
-def traffic_for(cfg):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary, if one matches."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        rec = json.load(open(path))
-    except Exception:
-        return None
-    for r in rec.get("records", []):
-        defaults = {"word_planes": 2}
-        if all(r.get(k, defaults.get(k, 1)) == cfg.get(k)
-               for k in ("size", "tb_depth", "rows_per_wave", "n_gpus", "streams", "word_planes")):
-            return r.get("hbm_bytes_per_launch")
-    return None
+    rec.update(info)
+    return rec
 
 
 def main():
@@ -110,17 +182,16 @@ def main():
     rule = pkg.REF_RULE if a.rule == "ref" else pkg.CONWAY
     n = a.size
     torch.cuda.set_device(local)
+    kw = dict(rule=rule, device=local, tb_depth=a.tb_depth, rows_per_wave=a.rows_per_wave,
+              handoff=a.handoff)
     if world > 1:
         dist.init_process_group("nccl")
         uid = [pkg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        eng = pkg.Engine(n, n, rule=rule, device=local, tb_depth=a.tb_depth,
-                         rows_per_wave=a.rows_per_wave, halo_depth=a.halo_depth,
-                         word_planes=a.word_planes,
-                         rank=rank, nranks=world, uid=uid[0])
+        eng = pkg.Engine(n, n, halo_depth=a.halo_depth, rank=rank, nranks=world, uid=uid[0],
+                         **kw)
     else:
-        eng = pkg.Engine(n, n, rule=rule, device=local, tb_depth=a.tb_depth,
-                         rows_per_wave=a.rows_per_wave, word_planes=a.word_planes)
+        eng = pkg.Engine(n, n, streams=a.streams, **kw)
     eng.init_random(a.seed)
 
     def barrier():
@@ -157,16 +228,20 @@ def main():
 
     cell_gens = float(n) * n * a.gens * a.steps
     gcups = cell_gens / dt / 1e9
-    # dominant kernel: the fused stencil; algorithmic bytes per launch =
-    # 0.25 B x (own cell-generations one launch produces)
+    # dominant kernel: the fused stencil (HIP events on each stripe's stream)
     cg_per_launch = tm["cell_gens"] / max(tm["launches"], 1)
     # a composite engine (gol_config.streams > 1) runs that many stripe launches
     # concurrently, each timed on its own stream: per-launch rate x streams
     streams = max(1, tm.get("streams", 1))
-    achieved = BYTES_PER_CELL_GEN * cg_per_launch * streams / (avg_launch_ms / 1e3) / 1e9
-    cfg_key = {"size": n, "tb_depth": eng.tb_depth, "rows_per_wave": a.rows_per_wave,
-               "n_gpus": world, "streams": streams, "word_planes": eng.word_planes}
-    traffic = traffic_for(cfg_key)
+    launch_s = avg_launch_ms / 1e3
+    peak_slot_rate = SIMDS * valu_peak_rate()  # wave-instruction slots / s
+    slots_per_launch = cg_per_launch / CELLS_PER_WAVE_INSTR * STAGE_SLOTS[a.rule]
+    valu_achieved = slots_per_launch * streams / launch_s
+    cfg_key = {"size": n, "rule": a.rule, "tb_depth": eng.tb_depth, "streams": streams,
+               "n_gpus": world, "rows_per_wave": eng.rows_per_wave, "handoff": eng.handoff}
+    ctr = counters_for(cfg_key) or {}
+    insts = ctr.get("insts_valu_per_launch")
+    traffic = ctr.get("hbm_bytes_per_launch")
 
     if rank == 0:
         rec = {
@@ -187,29 +262,41 @@ def main():
                 "h": n, "w": n, "gens_per_step": a.gens,
                 "rule": "B/S2 (reference effective rule)" if a.rule == "ref" else "B3/S23",
                 "tb_depth": eng.tb_depth, "word_planes": eng.word_planes,
-                "halo_depth": eng.halo_depth,
-                "rows_per_wave": eng.rows_per_wave,
+                "halo_depth": eng.halo_depth, "rows_per_wave": eng.rows_per_wave,
+                "handoff": eng.handoff,
                 "parallelism": f"row-stripes x{world}" if world > 1 else "single GPU",
             },
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "bound": "valu",
+                "achieved": round(valu_achieved / 1e9, 1),
+                "peak": round(peak_slot_rate / 1e9, 1),
+                "unit": "G VALU issue slots/s (stage logic: v_bitop3 1 slot, DPP move and "
+                        "v_alignbit 2 slots)",
+                "frac": round(valu_achieved / peak_slot_rate, 4),
                 "traffic": traffic,
                 "kernel": "life_tb_kernel",
                 "avg_launch_ms": round(avg_launch_ms, 4),
                 "launches": tm["launches"],
                 "concurrent_streams": streams,
-                "achieved_wall": round(BYTES_PER_CELL_GEN * gcups, 1),
                 "cell_gens_per_launch": cg_per_launch,
-                "bytes_per_cell_gen": BYTES_PER_CELL_GEN,
+                "work_ratio": round(tm["cell_gens_computed"] / max(tm["cell_gens"], 1), 4),
+                "valu": {
+                    "slots_per_word_gen": STAGE_SLOTS[a.rule],
+                    "insts_per_launch": insts,
+                    "issue_frac": (round(insts * streams / launch_s / peak_slot_rate, 4)
+                                   if insts else None),
+                    "peak_from": "profiles/r01/valu_rate.json (v_bitop3, 2 waves/SIMD, best "
+                                 "code placement) x 1024 SIMDs",
+                    "counters_from": "profiles/r02/counters.json" if insts else None,
+                },
+                "hbm_equiv_frac": round(BYTES_PER_CELL_GEN * gcups / HBM_PEAK_GBPS, 4),
+                "hbm_measured_frac": (round(traffic * streams / launch_s
+                                            / (HBM_PEAK_GBPS * 1e9), 4) if traffic else None),
             },
             "cpu_baseline": None,
         }
         if world == 1 and not a.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(a.cpu_threads, n)
+            rec["cpu_baseline"] = cpu_baseline(n, a.seed, a.cpu_threads)
         print(json.dumps(rec), flush=True)
     eng.close()
     if world > 1:

@@ -160,24 +160,33 @@ static void* bl_run(void* a)
     }
     return NULL;
 }
-/* Returns live-cell count (to keep the work observable). */
+static inline uint64_t splitmix64_at(uint64_t seed, uint64_t idx);
+
+/* Times the reference's algorithm on the benchmark's own field: thread t runs
+ * rows [t*rows_per_thread, (t+1)*rows_per_thread) of the w-wide synthetic field
+ * (cell (r, c) alive iff bit c%64 of splitmix64(seed, r*ceil(w/64) + c/64), as
+ * oracle_bp_init_random / the engine's gol_init_random) as its own stripe with a
+ * dead boundary, like one `mpirun -np threads` rank each.  Returns the live-cell
+ * count (keeps the work observable). */
 int64_t oracle_ref_baseline(int rows_per_thread, int w, int gens, int threads,
                             uint64_t seed, uint32_t birth, uint32_t survive)
 {
     bl_job* jobs = (bl_job*)calloc(threads, sizeof(bl_job));
     pthread_t* th = (pthread_t*)calloc(threads, sizeof(pthread_t));
-    uint64_t z = seed;
+    const uint64_t wq = ((uint64_t)w + 63) / 64;
     for (int t = 0; t < threads; t++) {
         jobs[t].rows = rows_per_thread; jobs[t].w = w; jobs[t].gens = gens;
         jobs[t].b = birth; jobs[t].s = survive;
         jobs[t].grid = (int32_t**)malloc(sizeof(int32_t*) * rows_per_thread);
         jobs[t].next = (int32_t**)malloc(sizeof(int32_t*) * rows_per_thread);
         for (int y = 0; y < rows_per_thread; y++) {
+            const uint64_t r = (uint64_t)t * (uint64_t)rows_per_thread + (uint64_t)y;
             jobs[t].grid[y] = (int32_t*)malloc(sizeof(int32_t) * w);
             jobs[t].next[y] = (int32_t*)calloc(w, sizeof(int32_t));
+            uint64_t word = 0;
             for (int x = 0; x < w; x++) {
-                z = z * 6364136223846793005ULL + 1442695040888963407ULL;
-                jobs[t].grid[y][x] = (z >> 63) ? LIVE_CELL : DEAD_CELL;
+                if ((x & 63) == 0) word = splitmix64_at(seed, r * wq + (uint64_t)(x >> 6));
+                jobs[t].grid[y][x] = ((word >> (x & 63)) & 1) ? LIVE_CELL : DEAD_CELL;
             }
         }
     }

@@ -135,3 +135,17 @@ def test_random_init_and_digest(oracle):
     # p = 0.5 on a bigger field
     big = oracle.bp_random(256, 4096, seed=1)
     assert abs(oracle.bp_digest(big, 4096)[0] / (256 * 4096) - 0.5) < 0.01
+
+
+def test_cpu_baseline_field_is_the_bench_field(oracle):
+    """bench.py's cpu_baseline times the reference algorithm on the benchmark's own
+    synthetic field: 0 generations leave exactly the live cells of the engine's
+    splitmix64 field (gol_init_random == oracle_bp_init_random)."""
+    for rows, w, threads in ((3, 200, 2), (5, 64, 3), (2, 65, 1)):
+        live = oracle.ref_baseline(rows, w, 0, threads, seed=1)
+        assert live == oracle.bp_digest(oracle.bp_random(rows * threads, w, 1), w)[0]
+    # and its stepping is the reference's (REF rule on each stripe alone)
+    g = oracle.bp_random(40, 90, 1)
+    want = sum(oracle.bp_digest(oracle.bp_run(g[t * 20:(t + 1) * 20], 90, 7), 90)[0]
+               for t in range(2))
+    assert oracle.ref_baseline(20, 90, 7, 2, seed=1) == want

@@ -4,26 +4,26 @@
 #      two stripe streams overlapping; the stats average must match bench.py's)
 #   B  SQ counters (VALU issue) of the default 65536^2 launches
 #   C/D FETCH_SIZE and WRITE_SIZE in their own passes (never combined with traces)
-#   E  hand-off A/B on the per-GPU shapes (no profiler)
+#   E  the bench line itself, with the CPU baseline (no profiler)
 # Each step has its own time limit; the first failure ends the script.
-# Usage: bash tools/gpu_profile_r02.sh TAG [extra profile_run.py args]
+# Usage: bash tools/gpu_profile_r02.sh TAG [args shared by bench.py and profile_run.py]
 set -e -o pipefail
 TAG=${1:-r02}; shift || true
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_traced.json 2> $OUT/trace.err
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $OUT/bench_traced.json 2> $OUT/trace.err
 echo "A done"
-timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVES \
+timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAIT_ANY \
     SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o pmc \
-    --output-format csv -- python3 tools/profile_run.py --launches 16 "$@" > $OUT/pmc_sq.log 2>&1
+    --output-format csv -- python3 tools/profile_run.py "$@" > $OUT/pmc_sq.log 2>&1
 echo "B done"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 180 rocprofv3 --pmc $C -d $OUT/pmc_$C -o pmc --output-format csv -- \
-      python3 tools/profile_run.py --launches 16 "$@" > $OUT/pmc_$C.log 2>&1
+      python3 tools/profile_run.py "$@" > $OUT/pmc_$C.log 2>&1
   echo "$C done"
 done
-timeout -k 10 300 python3 tools/ab_handoff.py > $OUT/ab_handoff.jsonl 2> $OUT/ab_handoff.err
-cat $OUT/ab_handoff.jsonl
+timeout -k 10 300 python3 bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
+cat $OUT/bench.json
 echo done > $OUT/DONE

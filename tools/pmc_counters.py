@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Turn tools/gpu_profile_r02.sh output into profiles/r02/counters.json records
+(read by bench.py's roofline):
+
+  insts_valu_per_launch  SQ_INSTS_VALU per life_tb_kernel launch (mean)
+  hbm_bytes_per_launch   FETCH_SIZE x f_read + WRITE_SIZE x f_write, the factors
+                         calibrated in the same run on kernels whose byte counts
+                         are known exactly (MI355X_MICROARCH.md §HBM):
+                           digest_kernel      reads  rows*wq*8 B, 8 B per lane
+                           init_random_kernel writes rows*stride*8 B, 8 B per lane
+  plus SQ_WAVE_CYCLES, SQ_WAIT_INST_ANY, GRBM_GUI_ACTIVE means and the effective
+  clock (GRBM_GUI_ACTIVE / 8 XCDs / mean kernel time from the kernel trace).
+
+    python tools/pmc_counters.py gpurun_out/prof_r02a --out profiles/r02/counters.json
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def per_kernel(path, counter):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        k = r["Kernel_Name"]
+        name = "life_tb_kernel" if "life_tb_kernel" in k else (
+            "digest_kernel" if "digest_kernel" in k else (
+                "init_random_kernel" if "init_random_kernel" in k else k))
+        out.setdefault(name, []).append(float(r["Counter_Value"]))
+    return out
+
+
+def config_of(log):
+    for line in open(log):
+        line = line.strip()
+        if line.startswith("{") and '"rows_per_wave"' in line:
+            return json.loads(line)
+    raise SystemExit(f"no configuration line in {log}")
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("prof_dir")
+    p.add_argument("--out", default="profiles/r02/counters.json")
+    a = p.parse_args()
+    d = a.prof_dir
+    cfg = config_of(os.path.join(d, "pmc_FETCH_SIZE.log"))
+    n, S = cfg["size"], cfg["streams"]
+    fetch = per_kernel(os.path.join(d, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(d, "pmc_WRITE_SIZE", "pmc_counter_collection.csv"), "WRITE_SIZE")
+    wq = (n + 63) // 64
+    stride = (wq + 7) // 8 * 8
+    # a composite engine runs digest / init per part, over 1/S of the rows each
+    f_read = n * wq * 8 / S / (statistics.mean(fetch["digest_kernel"]) * 1024)
+    f_write = n * stride * 8 / S / (statistics.mean(write["init_random_kernel"]) * 1024)
+    rd = statistics.mean(fetch["life_tb_kernel"]) * 1024 * f_read
+    wr = statistics.mean(write["life_tb_kernel"]) * 1024 * f_write
+    sq = os.path.join(d, "pmc_sq", "pmc_counter_collection.csv")
+    rec = dict(cfg)
+    for k in ("launches", "digest0", "digest"):
+        rec.pop(k, None)
+    rec.update({
+        "hbm_bytes_per_launch": round(rd + wr), "read_bytes_per_launch": round(rd),
+        "write_bytes_per_launch": round(wr),
+        "bytes_per_cell_gen_measured": round((rd + wr) * S / (n * n * cfg["tb_depth"]), 5),
+        "fetch_size_calibration": round(f_read, 4), "write_size_calibration": round(f_write, 4),
+    })
+    if os.path.exists(sq):
+        for c in ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                  "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE", "SQ_INSTS_SALU"):
+            v = per_kernel(sq, c).get("life_tb_kernel")
+            if v:
+                rec[c.lower() + "_per_launch"] = round(statistics.mean(v))
+        rec["insts_valu_per_launch"] = rec.get("sq_insts_valu_per_launch")
+        rec["launches_profiled"] = len(per_kernel(sq, "SQ_INSTS_VALU").get("life_tb_kernel", []))
+    stats = glob.glob(os.path.join(d, "trace", "*kernel_stats.csv"))
+    if stats:
+        for r in csv.DictReader(open(stats[0])):
+            if "life_tb_kernel" in r["Name"]:
+                rec["trace_avg_launch_ns"] = float(r["AverageNs"])
+                if rec.get("grbm_gui_active_per_launch"):
+                    rec["effective_clock_ghz"] = round(
+                        rec["grbm_gui_active_per_launch"] / 8 / float(r["AverageNs"]), 3)
+    rec["source"] = os.path.basename(os.path.normpath(d))
+    doc = {"records": []}
+    if os.path.exists(a.out):
+        doc = json.load(open(a.out))
+    keys = ("size", "rule", "tb_depth", "streams", "n_gpus", "rows_per_wave", "handoff")
+    doc["records"] = [r for r in doc["records"] if not all(r.get(k) == rec[k] for k in keys)]
+    doc["records"].append(rec)
+    doc["_doc"] = ("Per-launch counters of life_tb_kernel by configuration: rocprofv3 --pmc "
+                   "passes (FETCH_SIZE, WRITE_SIZE and the SQ set each in its own run) over "
+                   "tools/profile_run.py; see tools/pmc_counters.py")
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    json.dump(doc, open(a.out, "w"), indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()

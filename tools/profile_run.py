@@ -1,14 +1,19 @@
 #!/usr/bin/env python3
-"""Dev tool run under rocprofv3: a fixed sequence of kernels with known byte
-counts, so PMC counters can be calibrated for this access width (8 B per lane)
+"""Dev tool run under rocprofv3: the benchmark's default engine (or a variant)
+for a fixed number of full-depth launch rounds, plus kernels with known byte
+counts so PMC counters can be calibrated for this access width (8 B per lane)
 before pricing the stencil kernel (MI355X_MICROARCH.md §HBM: FETCH_SIZE is
 uncalibrated for widths other than 16 B/lane).
 
   init_random_kernel : writes exactly rows*stride*8 bytes (8 B/lane stores)
   digest_kernel      : reads exactly rows*wq*8 bytes (8 B/lane loads)
-  life_tb_kernel     : `launches` launches of depth K over the field
+  life_tb_kernel     : `launches` x tb_depth generations of the field
+
+Prints one JSON line with the engine's configuration (bench.py's record keys),
+which tools/pmc_counters.py reads back.
 """
 import argparse
+import json
 import os
 import sys
 
@@ -17,18 +22,25 @@ import __graft_entry__ as entry  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--size", type=int, default=65536)
+p.add_argument("--rule", default="ref", choices=["ref", "conway"])
 p.add_argument("--tb-depth", type=int, default=0, help="0 = the engine's auto layout")
-p.add_argument("--word-planes", type=int, default=0)
 p.add_argument("--rows-per-wave", type=int, default=0)
-p.add_argument("--launches", type=int, default=4)
+p.add_argument("--handoff", type=int, default=0)
+p.add_argument("--streams", type=int, default=0)
+p.add_argument("--launches", type=int, default=16)
 a = p.parse_args()
 pkg = entry.load_package()
-e = pkg.Engine(a.size, a.size, device=0, tb_depth=a.tb_depth, rows_per_wave=a.rows_per_wave,
-               word_planes=a.word_planes)
-print("layout", e.tb_depth, e.word_planes)
+rule = pkg.REF_RULE if a.rule == "ref" else pkg.CONWAY
+e = pkg.Engine(a.size, a.size, rule=rule, device=0, tb_depth=a.tb_depth,
+               rows_per_wave=a.rows_per_wave, handoff=a.handoff, streams=a.streams)
 e.init_random(1)
-print("digest", e.digest())
+d0 = e.digest()
+e.set_timing(1)
 e.step(e.tb_depth * a.launches)
 e.sync()
-print("digest", e.digest())
+tm = e.timing()
+print(json.dumps({"size": a.size, "rule": a.rule, "tb_depth": e.tb_depth,
+                  "streams": max(1, tm["streams"]), "n_gpus": 1,
+                  "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
+                  "launches": tm["launches"], "digest0": d0, "digest": e.digest()}))
 e.close()
