@@ -131,9 +131,9 @@ def host_info():
 
 def cpu_baseline(w, seed, threads=0):
     """Oracle port of the reference algorithm (int per cell, per-cell neighbour
-    loop) on the benchmark's own field: `threads` stripes of 256 rows x w columns
-    (rows [0, threads*256) of the splitmix64 field), each evolved alone like one
-    `mpirun -np threads` rank, E = 32 generations of B/S2; GCUPS from
+    loop) on the benchmark's own field: `threads` stripes of 512 rows x w columns
+    (rows [0, threads*512) of the splitmix64 field), each evolved alone like one
+    `mpirun -np threads` rank, E = 64 generations of B/S2; GCUPS from
     T(E) - T(0), so building the field is not counted."""
     info = host_info()
     if not threads:
@@ -142,7 +142,7 @@ def cpu_baseline(w, seed, threads=0):
         if omp and omp.isdigit():  # the box's CPU share (set there)
             threads = min(threads, int(omp))
     orc = entry.load_oracle()
-    rows, gens = 256, 32
+    rows, gens = 512, 64
     t0 = time.perf_counter()
     orc.ref_baseline(rows, w, 0, threads, seed)
     t_init = time.perf_counter() - t0

@@ -90,6 +90,15 @@ typedef struct gol_config {
     uint32_t word_planes;  /* cell planes per lane: 0 = auto (= 2: one word = 64
                               columns per lane); 4 (two words per lane) exists
                               only in the dev build (make dev) */
+    uint32_t resident;     /* gol_create, GLOBAL only: small fields held in
+                              registers across the chip and advanced by ONE
+                              launch per gol_step (tiles swap halo rows every K
+                              generations inside the launch); 0 = auto (when the
+                              field fits and no streaming-kernel knob --
+                              tb_depth, rows_per_wave, handoff, strip_lanes,
+                              word_planes -- is set), 1 = off, 2 = on if the
+                              field fits (then tb_depth sets K and rows_per_wave
+                              the rows each wavefront holds: 2,3,4,6,8) */
 } gol_config;
 
 typedef struct gol_engine gol_engine;
@@ -165,6 +174,9 @@ gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_pe
 
 /* Whether full-depth launches use hand-off row blocks (gol_config.handoff, as
  * the planner resolved it): 1 = yes, 0 = every block recomputes its halo. */
+/* Resident plan (gol_config.resident): *on = 1 if gol_step runs the resident
+ * kernel; then *bands x *strips tiles, one workgroup each. */
+gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint32_t* strips);
 gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff);
 
 /* ---- Multi-GPU, one process per GPU (replaces the MPI stripes :70-81 and the

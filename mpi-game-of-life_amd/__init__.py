@@ -34,6 +34,7 @@ EXPORTS = [
     "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
     "gol_create_rank", "gol_create_group", "gol_group_step", "gol_plan_info",
     "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
+    "gol_plan_resident",
 ]
 
 
@@ -57,6 +58,7 @@ class Config(ctypes.Structure):
         ("streams", ctypes.c_uint32),
         ("strip_lanes", ctypes.c_uint32),
         ("word_planes", ctypes.c_uint32),
+        ("resident", ctypes.c_uint32),
     ]
 
 
@@ -146,6 +148,7 @@ def lib():
     L.gol_group_step.argtypes = [ctypes.POINTER(vp), i32, u64]
     L.gol_plan_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.gol_plan_handoff.argtypes = [vp, ctypes.POINTER(u32)]
+    L.gol_plan_resident.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.gol_create_rank_transport.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32,
                                             ctypes.POINTER(Transport), ctypes.POINTER(vp)]
     L.gol_round_schedule.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32, u64, i32,
@@ -156,6 +159,7 @@ def lib():
                  "gol_sync", "gol_digest", "gol_set_timing", "gol_get_timing",
                  "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
                  "gol_create_group", "gol_group_step", "gol_plan_info", "gol_plan_handoff",
+                 "gol_plan_resident",
                  "gol_create_rank_transport", "gol_round_schedule"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -169,7 +173,7 @@ def _check(st):
 
 def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_depth=0,
                 halo_depth=0, rows_per_wave=0, handoff=0, streams=0, strip_lanes=0,
-                word_planes=0):
+                word_planes=0, resident=0):
     c = Config()
     lib().gol_config_init(ctypes.byref(c))
     c.birth_mask, c.survive_mask = rule
@@ -183,6 +187,7 @@ def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_
     c.streams = streams
     c.strip_lanes = strip_lanes
     c.word_planes = word_planes
+    c.resident = resident
     return c
 
 
@@ -223,7 +228,7 @@ class Engine:
     def __init__(self, h, w, rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1,
                  tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None,
                  handoff=0, streams=0, strip_lanes=0, word_planes=0, transport=None,
-                 _handle=None):
+                 resident=0, _handle=None):
         """transport: for a rank engine, a callable (send_up, send_down) -> (recv_up,
         recv_down) of bytes objects (None where there is no neighbour) used instead
         of RCCL (gol_create_rank_transport)."""
@@ -231,7 +236,7 @@ class Engine:
         self.wq = (w + 63) // 64
         self._tp = None
         cfg = make_config(rule, device, semantics, ref_ranks, tb_depth, halo_depth,
-                          rows_per_wave, handoff, streams, strip_lanes, word_planes)
+                          rows_per_wave, handoff, streams, strip_lanes, word_planes, resident)
         handle = ctypes.c_void_p()
         if _handle is not None:
             handle = _handle
@@ -262,6 +267,10 @@ class Engine:
         ho = ctypes.c_uint32()
         _check(lib().gol_plan_handoff(self._h, ctypes.byref(ho)))
         self.handoff = bool(ho.value)
+        on, nb, ns = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().gol_plan_resident(self._h, ctypes.byref(on), ctypes.byref(nb), ctypes.byref(ns)))
+        # resident kernel: (bands, strips) of its tiles, or None
+        self.resident = (nb.value, ns.value) if on.value else None
 
     def close(self):
         if self._h:

@@ -222,6 +222,16 @@ struct gol_engine {
     uint32_t* flags[2] = {nullptr, nullptr};
     int* d_err = nullptr;
 
+    // resident kernel (life_resident.hip): small GLOBAL fields, one launch per
+    // gol_step; flags count the epochs published, from flag_base on
+    struct Resident {
+        bool on = false;
+        int rows = 0;  // rows per wavefront
+        int32_t strips = 0, bands = 0, band_rows = 0, K = 0;
+        uint32_t* flags = nullptr;
+        uint32_t flag_base = 0;
+    } res;
+
     std::vector<Region> user_regions;  // load/store mapping (own output rows)
     std::vector<Region> load_regions;  // rows loaded (REF_STRIPES loads overlaps too)
 
@@ -292,8 +302,8 @@ bool handoff_fits(int64_t R, int d, int planes) { return gol::handoff_toff(R, d,
 // A wavefront's time in rows of K stage-steps: classic blocks R + K + 1 (+ c0
 // fixed); hand-off blocks skip the K - 1 rows of vertical halo but their steady
 // loop runs ~4% slower per row (bigger code, side-row refills):
-// 1.04 R + 8, fitted to the in-process A/B of profiles/r02/ab_handoff_*.jsonl
-// (8448 rows: hand-off 5% faster; 33024 / 65536 rows: classic 1-3% faster).  Measured
+// 1.04 R + 12, fitted to the in-process A/B of profiles/r02/ab_handoff_shapes.jsonl
+// (8448 rows: hand-off 5% faster; 33024 / 65536 rows: classic 1-4% faster).  Measured
 // (profiles/r01/sweep_rows_per_wave*.jsonl): keeping fewer than `occ`
 // wavefronts per SIMD all launch long is 5-10% slower than the model says, so R
 // is restricted to n >= occ whenever the field is large enough.  Narrower strips
@@ -338,7 +348,7 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
                 const int64_t full = n / occ, rem = n % occ;
                 const double slots =
                     (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
-                const double rows = hand ? 1.04 * (double)R + 8.0 : (double)(R + K + 1 + c0);
+                const double rows = hand ? 1.04 * (double)R + 12.0 : (double)(R + K + 1 + c0);
                 const double cost = slots * rows;
                 const int filled = n >= occ ? 1 : 0;
                 if (cost < best[hand][filled] * 0.999) {
@@ -368,12 +378,22 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                           : 0;
     int64_t max_units = 0;
     bool any_hand = false;
+    // hand-off or classic blocks for the whole engine, decided on its widest plan
+    // (all launches of a step then share one kernel kind; a plan where hand-off
+    // does not fit still falls back to classic blocks)
+    uint32_t handoff = e->handoff;
+    if (handoff == 0 && !raw.empty())
+        handoff = pick_rows_per_wave(raw[0], e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
+                                     (int)e->rows_per_wave, e->lane_shift, 0)
+                          .hand
+                      ? 2
+                      : 1;
     for (size_t pi = 0; pi < raw.size(); ++pi) {
         const auto& r = raw[pi];
         gol_engine::Plan p;
         p.segs = r;
         const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
-                                              (int)e->rows_per_wave, e->lane_shift, e->handoff);
+                                              (int)e->rows_per_wave, e->lane_shift, handoff);
         p.rpw = rp.rpw;
         p.groups = rp.groups;
         p.lane_shift = rp.lane_shift;
@@ -437,6 +457,7 @@ gol_status check_cfg(const gol_config* cfg)
         cfg->strip_lanes != 16)
         return fail(GOL_EINVAL, "strip_lanes must be 0 (auto), 64, 32 or 16");
     if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
+    if (cfg->resident > 2) return fail(GOL_EINVAL, "resident must be 0 (auto), 1 (off) or 2 (on)");
     if (cfg->word_planes != 0 && cfg->word_planes != 2 && cfg->word_planes != 4)
         return fail(GOL_EINVAL, "word_planes must be 0 (auto), 2 or 4");
     if (cfg->word_planes == 4 && !gol::kDevKernels)
@@ -561,6 +582,8 @@ void step_schedule(uint32_t K, uint64_t Hx, bool overlap, bool halo_fresh, uint6
     }
 }
 
+gol_status plan_resident(gol_engine* e, const gol_config* cfg);
+
 // Common construction; geometry (row0, R, Hx, rank) already set.
 gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* cfg,
                        const RankGeom* geom)
@@ -667,6 +690,8 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
     HIP_TRY(hipMalloc(&e->d_flag, sizeof(int)));
     gol_status st = build_plans(e, raw);
     if (st != GOL_OK) return st;
+    st = plan_resident(e, cfg);
+    if (st != GOL_OK) return st;
     HIP_TRY(hipStreamSynchronize(e->stream));
     return GOL_OK;
 }
@@ -702,6 +727,125 @@ gol_status get_event(gol_engine* e, hipEvent_t* ev)
     return GOL_OK;
 }
 
+// HIP events around every `timing_every`-th kernel launch (gol_set_timing).
+gol_status timing_begin(gol_engine* e, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1)
+{
+    *e0 = *e1 = nullptr;
+    if (!e->timing_every || (e->launch_count++ % e->timing_every) != 0) return GOL_OK;
+    GOL_TRY(get_event(e, e0));
+    GOL_TRY(get_event(e, e1));
+    HIP_TRY(hipEventRecord(*e0, s));
+    return GOL_OK;
+}
+
+gol_status timing_end(gol_engine* e, hipStream_t s, hipEvent_t e0, hipEvent_t e1, double own,
+                      double computed)
+{
+    if (!e0) return GOL_OK;
+    HIP_TRY(hipEventRecord(e1, s));
+    e->ev_pending.push_back({e0, e1});
+    e->pending_cells.push_back(own);
+    e->pending_cells_comp.push_back(computed);
+    return GOL_OK;
+}
+
+// Resident plan: tiles of `band_rows` rows x one 64-lane strip, one 1024-thread
+// workgroup each (at most one per CU: every workgroup of the launch must be
+// resident at once, since tiles wait for their neighbours), each wavefront
+// holding `rows` rows, so a tile holds 16 rows x band + 2K halo rows.  Cost per
+// generation, in us: 0.03 + 0.025 rows (a workgroup barrier and 16 wavefronts
+// of rows + 2 H3 rows and rows rule rows on 4 SIMDs) + 2.0 / K (one flag
+// hand-off per epoch, MI355X_MICROARCH.md price list: handoff-flag).
+gol_status plan_resident(gol_engine* e, const gol_config* cfg)
+{
+    if (cfg->resident == 1 || e->nranks > 1 || e->sem != GOL_SEM_GLOBAL || e->planes != 2)
+        return GOL_OK;
+    const bool knobs = cfg->tb_depth || cfg->rows_per_wave || cfg->handoff || cfg->strip_lanes ||
+                       cfg->word_planes;
+    if (cfg->resident == 0 && knobs) return GOL_OK;
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
+    const int64_t strips = e->ng <= 64 ? 1 : ((int64_t)e->ng + 61) / 62;
+    if (strips > cus) return GOL_OK;
+    const int64_t h = (int64_t)e->H;
+    double best = 1e300;
+    for (int M : gol::kResRowsList) {
+        if (cfg->resident == 2 && cfg->rows_per_wave && (uint32_t)M != cfg->rows_per_wave) continue;
+        if (gol::resident_blocks_per_cu(M, e->rule) < 1) continue;
+        const int64_t NR = (int64_t)gol::kResWaves * M;
+        const int64_t max_bands = std::min<int64_t>(cus / strips, h);
+        for (int64_t nb = 1; nb <= max_bands; ++nb) {
+            const int64_t B = (h + nb - 1) / nb;
+            const int64_t bands = (h + B - 1) / B;
+            int64_t kmax = (NR - B) / 2;
+            if (strips > 1) kmax = std::min<int64_t>(kmax, 63);
+            int64_t K = (cfg->resident == 2 && cfg->tb_depth) ? (int64_t)cfg->tb_depth : kmax;
+            if (K < 1 || K > kmax || (cfg->resident == 0 && K < 8)) continue;
+            const int64_t span = (K + B - 1) / B;  // bands a K-row halo reaches
+            if ((2 * span + 1) * (strips > 1 ? 3 : 1) - 1 > 64) continue;
+            const double cost = 0.03 + 0.025 * M + 2.0 / (double)K;
+            if (cost < best * 0.999) {
+                best = cost;
+                e->res.rows = M;
+                e->res.strips = (int32_t)strips;
+                e->res.bands = (int32_t)bands;
+                e->res.band_rows = (int32_t)B;
+                e->res.K = (int32_t)K;
+            }
+        }
+    }
+    if (best >= 1e300) {
+        if (cfg->resident == 2 && (cfg->tb_depth || cfg->rows_per_wave))
+            return fail(GOL_EINVAL, "resident: the field does not fit with this tb_depth / rows_per_wave");
+        return GOL_OK;
+    }
+    const size_t tiles = (size_t)e->res.bands * (size_t)e->res.strips;
+    HIP_TRY(hipMalloc(&e->res.flags, tiles * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(e->res.flags, 0, tiles * sizeof(uint32_t)));
+    e->res.on = true;
+    e->K = (uint32_t)e->res.K;
+    return GOL_OK;
+}
+
+// gol_step on a resident engine: one launch (per 2^30 generations).
+gol_status step_resident(gol_engine* e, uint64_t generations)
+{
+    auto& r = e->res;
+    uint64_t left = generations;
+    while (left > 0) {
+        const int32_t g = (int32_t)std::min<uint64_t>(left, 1u << 30);
+        gol::ResArgs a{};
+        a.buf0 = e->buf[e->cur];
+        a.buf1 = e->buf[e->cur ^ 1];
+        a.flags = r.flags;
+        a.err = e->d_err;
+        a.stride = (int64_t)e->stride;
+        a.h = (int64_t)e->H;
+        a.ng = (int64_t)e->ng;
+        a.lastmask = e->lastmask_split[0];
+        a.strips = r.strips;
+        a.bands = r.bands;
+        a.band_rows = r.band_rows;
+        a.K = r.K;
+        a.span = (r.K + r.band_rows - 1) / r.band_rows;
+        a.gens = g;
+        a.flag_base = r.flag_base;
+        a.birth = e->birth;
+        a.survive = e->survive;
+        hipEvent_t e0, e1;
+        GOL_TRY(timing_begin(e, e->stream, &e0, &e1));
+        HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, e->stream));
+        // lanes process every held row of every tile, every generation
+        const double comp = (double)g * r.bands * r.strips * gol::kResWaves * r.rows * 64.0 * 64.0;
+        GOL_TRY(timing_end(e, e->stream, e0, e1, (double)e->H * (double)e->W * g, comp));
+        const uint32_t epochs = (uint32_t)((g + r.K - 1) / r.K);
+        r.flag_base += epochs;
+        if (epochs & 1) e->cur ^= 1;
+        left -= (uint64_t)g;
+    }
+    return GOL_OK;
+}
+
 gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
                   hipStream_t stream = nullptr)
 {
@@ -732,18 +876,10 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         a.side_slot = (int64_t)2 * (depth - 1) * 64 * (e->planes / 2);
         a.tail_off = gol::handoff_toff(p.rpw, (int)depth, e->planes);
     }
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    const bool timed = e->timing_every && (e->launch_count++ % e->timing_every) == 0;
-    if (timed) {
-        gol_status st = get_event(e, &e0);
-        if (st == GOL_OK) st = get_event(e, &e1);
-        if (st != GOL_OK) return st;
-        HIP_TRY(hipEventRecord(e0, s));
-    }
+    hipEvent_t e0, e1;
+    GOL_TRY(timing_begin(e, s, &e0, &e1));
     HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->planes, hand, s));
-    if (timed) {
-        HIP_TRY(hipEventRecord(e1, s));
-        e->ev_pending.push_back({e0, e1});
+    if (e0) {
         // cell-generations the lanes actually process: every stage of a block
         // computes its rows, a classic block (and the last block of a hand-off
         // segment) also d(d-1) stage-rows of vertical halo, and every strip also
@@ -755,8 +891,7 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
             comp += depth * n + classic * depth * (depth - 1.0);
         }
         const double cols = (double)p.groups * 64.0 * 32.0 * e->planes;
-        e->pending_cells.push_back(p.own_rows * (double)e->W * depth);
-        e->pending_cells_comp.push_back(comp * cols);
+        GOL_TRY(timing_end(e, s, e0, e1, p.own_rows * (double)e->W * depth, comp * cols));
     }
     if (swap) e->cur ^= 1;
     return GOL_OK;
@@ -809,7 +944,7 @@ gol_status check_err(gol_engine* e)
             }();
             HIP_TRY(hipMemset(e->flags[r], 0, (size_t)n * sizeof(uint32_t)));
         }
-    return fail(GOL_EHIP, "row-block hand-off wait timed out in the stencil kernel; "
+    return fail(GOL_EHIP, "a wait for a neighbour's rows timed out in the stencil kernel; "
                           "the field is not valid");
 }
 
@@ -1170,6 +1305,7 @@ void gol_destroy(gol_engine* e)
         if (e->flags[b]) (void)hipFree(e->flags[b]);
     }
     if (e->d_err) (void)hipFree(e->d_err);
+    if (e->res.flags) (void)hipFree(e->res.flags);
     for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.exec);
     if (e->d_acc) (void)hipFree(e->d_acc);
     if (e->d_flag) (void)hipFree(e->d_flag);
@@ -1471,6 +1607,7 @@ gol_status run_launch_op(gol_engine* e, const SchedOp& op, Xchg&& xchg)
 // starting buffer).
 gol_status step_single(gol_engine* e, uint64_t generations)
 {
+    if (e->res.on) return step_resident(e, generations);
     uint64_t left = generations;
     const bool graphable = e->timing_every == 0 && generations >= 4 * (uint64_t)e->K;
     if (graphable) {
@@ -1760,7 +1897,9 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uin
         if (rows) *rows = e->H;
         return GOL_OK;
     }
-    if (rows_per_wave) *rows_per_wave = e->plans.empty() ? 0 : (uint32_t)e->plans.back().rpw;
+    if (rows_per_wave)
+        *rows_per_wave = e->res.on ? (uint32_t)e->res.rows
+                                   : e->plans.empty() ? 0 : (uint32_t)e->plans.back().rpw;
     if (h) *h = e->H;
     if (w) *w = e->W;
     if (row0) *row0 = e->row0;
@@ -1780,8 +1919,23 @@ gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_pe
     if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
     // rank engines: plans[Hx-1] is the full-round launch over own rows; else plans[0]
     const auto& p = e->nranks > 1 ? e->plans[e->Hx - 1] : e->plans[0];
-    if (strip_lanes) *strip_lanes = (uint32_t)(64 >> p.lane_shift);
-    if (rows_per_wave) *rows_per_wave = (uint32_t)p.rpw;
+    if (strip_lanes) *strip_lanes = e->res.on ? 64u : (uint32_t)(64 >> p.lane_shift);
+    if (rows_per_wave) *rows_per_wave = e->res.on ? (uint32_t)e->res.rows : (uint32_t)p.rpw;
+    return GOL_OK;
+}
+
+gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint32_t* strips)
+{
+    if (!e || !on) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) {
+        *on = 0;
+        if (bands) *bands = 0;
+        if (strips) *strips = 0;
+        return GOL_OK;
+    }
+    *on = e->res.on ? 1u : 0u;
+    if (bands) *bands = (uint32_t)e->res.bands;
+    if (strips) *strips = (uint32_t)e->res.strips;
     return GOL_OK;
 }
 
@@ -1791,7 +1945,7 @@ gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff)
     if (!e->parts.empty()) return gol_plan_handoff(e->parts[0], handoff);
     if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
     const auto& p = e->nranks > 1 ? e->plans[e->Hx - 1] : e->plans[0];
-    *handoff = (p.hand && p.multi_blk && e->side[0] && handoff_fits(p.rpw, (int)e->K, e->planes))
+    *handoff = (!e->res.on && p.hand && p.multi_blk && e->side[0] && handoff_fits(p.rpw, (int)e->K, e->planes))
                    ? 1u
                    : 0u;
     return GOL_OK;

@@ -123,6 +123,35 @@ hipError_t launch_depth(const StepArgs& a, RuleKind rule, int planes, bool hand,
 template <int K>
 int occupancy_depth(RuleKind rule, int planes, bool hand);
 
+// The resident kernel (life_resident.hip): one launch runs a whole gol_step on a
+// small field held in registers by one 1024-thread workgroup per (band, strip)
+// tile; neighbouring tiles swap their band rows every K generations through
+// the two field buffers (epoch e's result in buf0 if e is even, else buf1;
+// buf0 holds the input).
+constexpr int kResWaves = 16;                     // wavefronts per workgroup
+constexpr int kResRowsList[] = {2, 3, 4, 6, 8};   // rows per wavefront (instantiated)
+struct ResArgs {
+    uint64_t* buf0;       // row 0 of the input buffer (also the even epochs' output)
+    uint64_t* buf1;
+    uint32_t* flags;      // one per tile: epochs published, counting from flag_base
+    int* err;             // set when a neighbour wait timed out
+    int64_t stride;       // words per buffer row
+    int64_t h;            // field rows
+    int64_t ng;           // lane groups (= words) per row
+    uint64_t lastmask;    // stored-form valid bits of group ng - 1
+    int32_t strips;       // 1: lane l = group l (ng <= 64); else 62 groups + 2 halo lanes
+    int32_t bands;
+    int32_t band_rows;    // B; tiles hold B + 2K <= kResWaves * M rows
+    int32_t K;            // generations per epoch (<= 63 when strips > 1)
+    int32_t span;         // ceil(K / band_rows): bands a halo reaches; (2 span + 1) x
+                          // (strips > 1 ? 3 : 1) - 1 <= 64 neighbour tiles
+    int32_t gens;         // generations of this launch
+    uint32_t flag_base;
+    uint32_t birth, survive;
+};
+hipError_t launch_resident(const ResArgs& a, int rows, RuleKind rule, int grid, hipStream_t s);
+int resident_blocks_per_cu(int rows, RuleKind rule);
+
 // Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field
 // rows [glob_row0, glob_row0+nrows).
 hipError_t launch_init_random(uint64_t* buf, int64_t stride, int64_t wq, uint64_t lastmask,

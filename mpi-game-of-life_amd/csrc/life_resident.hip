@@ -1,0 +1,262 @@
+// life_resident.hip -- the resident kernel: small fields advanced for a whole
+// gol_step in ONE launch, the field held in registers across the chip.
+//
+// Same per-generation update as life_tb_kernel (Parallel_Life_MPI.cpp
+// countNeighbours :16-35 + updateGrid :37-54 on the bit-packed lane groups of
+// bitlayout.h, bit-sliced H3 sums and the rule32_total LUT logic of
+// life_stencil.h), but laid out for fields of a few thousand rows (SURVEY C2,
+// 4096^2 x 1000), where the streaming kernel is latency-bound: a launch of K
+// fused generations there is a ~20-step load/compute chain per wavefront plus
+// a kernel boundary, ~1.3 us per generation in all.
+//
+// Layout.  The field is cut into bands (row ranges of B rows) x strips (64-lane
+// column strips; one strip of up to 64 lane groups covers the whole row with no
+// halo lanes, wider rows use strips of 62 groups + 2 halo lanes as the
+// streaming kernel does).  One 1024-thread workgroup per (band, strip), at most
+// one per CU: its 16 wavefronts hold M consecutive rows each in VGPRs, rows
+// [b0 - K, b0 - K + 16 M) ⊇ [b0 - K, b1 + K), the band plus K halo rows on each
+// side.  A generation is: every wavefront puts its first and last row in LDS,
+// one workgroup barrier, it reads the row above its first and below its last,
+// and computes its M rows in registers.  Rows at the edge of the held range are
+// wrong by one more row per generation, so after K generations exactly the
+// band is valid: an epoch.
+//
+// Between epochs (every K generations) a workgroup publishes its band rows to
+// the ping-pong field buffer of the next epoch (write-through sc1 stores), then
+// one lane an sc1 flag = epoch count; it waits for the flags of its neighbours
+// (the bands within K rows above and below, in its own strip and the strips
+// left and right) and reloads
+// its halo rows and halo lanes from that buffer with sc1 loads
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first table row: sc1
+// payload, every storing wave's vmcnt(0) behind a workgroup barrier, one sc1
+// flag store per workgroup; the polling wave loads after its poll matched, the
+// others after the barrier it joins; hipMalloc buffers, one workgroup per CU --
+// enforced by the 96 KB of LDS each workgroup allocates).  Flags only grow:
+// the host passes the count reached by earlier launches as flag_base.  Ping-pong
+// safety: a workgroup overwrites the buffer of epoch e only in epoch e + 2,
+// after its neighbours' epoch e+1 flags, which they publish after reading it.
+// Waits are bounded: a timeout sets *err and the launch still drains.
+#include "life_stencil.h"
+
+namespace gol {
+
+namespace {
+
+constexpr int kResLdsWords = 96 * 1024 / 8;  // > 80 KB: one workgroup per CU
+static_assert(2 * 2 * kResWaves * 64 <= kResLdsWords, "edge rows fit the LDS block");
+
+// H3 of a row: bit-sliced sum (s) and carry (c) of each cell and its 2
+// horizontal neighbours (life_stencil.h stage_step's first half).
+__device__ __forceinline__ void h3_row(const Pl<2>& x, Pl<2>& s, Pl<2>& c)
+{
+    const Ends e = ends(x);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t L = left_of(x, e, k), R = right_of(x, e, k);
+        s.v[k] = lop3<kXor3>(L, x.v[k], R);
+        c.v[k] = lop3<kMaj>(L, x.v[k], R);
+    }
+}
+
+__device__ __forceinline__ Pl<2> zero_pl()
+{
+    Pl<2> z;
+    z.v[0] = z.v[1] = 0u;
+    return z;
+}
+
+__device__ __forceinline__ Pl<2> load_pl(const uint64_t* p)
+{
+    return planes_of<2>(load_grp<2>(p));
+}
+
+template <int M, int RULE>
+__global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
+{
+    constexpr bool kBirths = RULE != RULE_REF;
+    constexpr int W = kResWaves;
+    __shared__ uint64_t lds[kResLdsWords];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+    // workgroup -> tile; consecutive tiles on blocks b, b + 8, ... which share an
+    // XCD under round-robin dispatch (speed only, never correctness)
+    const int G = (int)gridDim.x;
+    int tile = (int)blockIdx.x;
+    if ((G & 7) == 0) tile = (tile & 7) * (G >> 3) + (tile >> 3);
+    const int band = tile / a.strips, strip = tile % a.strips;
+    const int64_t b0 = (int64_t)band * a.band_rows;
+    const int64_t b1 = min(b0 + a.band_rows, a.h);
+    const int64_t r0 = b0 - a.K + (int64_t)wv * M;  // field row of this wave's x[0]
+
+    // lane group of this lane
+    const bool multi = a.strips > 1;
+    const int64_t gi = multi ? (int64_t)strip * 62 - 1 + lane : lane;
+    const bool lane_ok = gi >= 0 && gi < a.ng;
+    const bool halo_lane = multi && (lane == 0 || lane == 63);
+    const bool st_lane = lane_ok && !halo_lane;
+    Pl<2> cm;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        cm.v[k] = lane_ok ? (gi == a.ng - 1 ? (uint32_t)(a.lastmask >> (32 * k)) : ~0u) : 0u;
+    const uint32_t voff = (uint32_t)((lane_ok ? gi : 0) * 8);
+
+    auto row_ptr = [&](const uint64_t* buf, int64_t r) -> const uint64_t* {
+        return reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(buf + r * a.stride) +
+                                                 voff);
+    };
+    auto fetch = [&](const uint64_t* buf, int64_t r) -> Pl<2> {
+        if (r < 0 || r >= a.h || !lane_ok) return zero_pl();
+        Pl<2> x = load_pl(row_ptr(buf, r));
+        x.v[0] &= cm.v[0];
+        x.v[1] &= cm.v[1];
+        return x;
+    };
+
+    Pl<2> x[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] = fetch(a.buf0, r0 + i);
+    // rows of the held range outside the field stay dead (rules with births)
+    uint32_t rowm[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) rowm[i] = (r0 + i >= 0 && r0 + i < a.h) ? ~0u : 0u;
+
+    // the neighbour tiles whose flags this workgroup waits for: bands within
+    // a.span = ceil(K / B) (a K-row halo can reach that far), strips within 1;
+    // lanes of wave 0 poll one each (the host keeps the count <= 64)
+    int nb_tile = -1;
+    if (wv == 0) {
+        const int sw = multi ? 3 : 1;
+        const int center = a.span * sw + sw / 2;
+        const int j = lane + (lane >= center ? 1 : 0);
+        if (j < (2 * a.span + 1) * sw) {
+            const int nbd = band + j / sw - a.span, nst = strip + j % sw - sw / 2;
+            if (nbd >= 0 && nbd < a.bands && nst >= 0 && nst < a.strips)
+                nb_tile = nbd * a.strips + nst;
+        }
+    }
+
+    uint32_t epoch = 0;
+    bool gave_up = false;
+    for (int32_t done = 0; done < a.gens;) {
+        const int32_t k = min(a.K, a.gens - done);
+        for (int32_t g = 0; g < k; ++g) {
+            uint64_t* ed = lds + (g & 1) * (2 * W * 64);  // [top/bottom][wave][lane]
+            Pl<2> up = zero_pl(), dn = zero_pl();
+            if constexpr (!(GOL_EXP & 32)) {
+                ed[wv * 64 + lane] = words_of<2>(x[0]).w[0];
+                ed[(W + wv) * 64 + lane] = words_of<2>(x[M - 1]).w[0];
+                if constexpr (!(GOL_EXP & 16)) __syncthreads();
+                if (wv > 0) up = planes_of<2>(Grp<2>{{ed[(W + wv - 1) * 64 + lane]}});
+                if (wv < W - 1) dn = planes_of<2>(Grp<2>{{ed[(wv + 1) * 64 + lane]}});
+            }
+            Pl<2> s[M + 2], c[M + 2];
+            h3_row(up, s[0], c[0]);
+#pragma unroll
+            for (int i = 0; i < M; ++i) h3_row(x[i], s[i + 1], c[i + 1]);
+            h3_row(dn, s[M + 1], c[M + 1]);
+#pragma unroll
+            for (int i = 0; i < M; ++i) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    uint32_t y = rule32_total<RULE>(s[i].v[q], c[i].v[q], s[i + 1].v[q], c[i + 1].v[q],
+                                                    s[i + 2].v[q], c[i + 2].v[q], x[i].v[q], a.birth,
+                                                    a.survive);
+                    if constexpr (kBirths) y = lop3<kAnd3>(y, cm.v[q], rowm[i]);
+                    x[i].v[q] = y;
+                }
+            }
+        }
+        done += k;
+        ++epoch;
+        // publish the band rows into the buffer of this epoch's result
+        uint64_t* nb = (epoch & 1) ? a.buf1 : a.buf0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const int64_t r = r0 + i;
+            if (r >= b0 && r < b1 && st_lane)
+                __hip_atomic_store(const_cast<uint64_t*>(row_ptr(nb, r)), words_of<2>(x[i]).w[0],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t want = a.flag_base + epoch;
+        if (threadIdx.x == 0)
+            __hip_atomic_store(a.flags + tile, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done >= a.gens) break;
+        // wait for the neighbours' rows of this epoch
+        if (nb_tile >= 0 && !gave_up && !(GOL_EXP & 64)) {
+            int n = 0;
+            while ((int32_t)(__hip_atomic_load(a.flags + nb_tile, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) -
+                             want) < 0) {
+                if (++n > kPollLimit) {  // the field is lost: flag it, stop waiting
+                    __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    gave_up = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        // reload the halo rows (all lanes) and the halo lanes of the band rows
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const int64_t r = r0 + i;
+            const bool own = r >= b0 && r < b1;
+            if (!own || halo_lane) x[i] = fetch(nb, r);
+        }
+    }
+}
+
+template <int M>
+hipError_t launch_res_m(const ResArgs& a, RuleKind rule, int grid, hipStream_t s)
+{
+    switch (rule) {
+    case RULE_REF: hipLaunchKernelGGL((life_res_kernel<M, RULE_REF>), dim3(grid), dim3(64 * kResWaves), 0, s, a); break;
+    case RULE_CONWAY: hipLaunchKernelGGL((life_res_kernel<M, RULE_CONWAY>), dim3(grid), dim3(64 * kResWaves), 0, s, a); break;
+    default: hipLaunchKernelGGL((life_res_kernel<M, RULE_GENERIC>), dim3(grid), dim3(64 * kResWaves), 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+template <int M>
+int occupancy_res_m(RuleKind rule)
+{
+    int n = 0;
+    hipError_t e;
+    switch (rule) {
+    case RULE_REF: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, life_res_kernel<M, RULE_REF>, 64 * kResWaves, 0); break;
+    case RULE_CONWAY: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, life_res_kernel<M, RULE_CONWAY>, 64 * kResWaves, 0); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, life_res_kernel<M, RULE_GENERIC>, 64 * kResWaves, 0); break;
+    }
+    return e == hipSuccess ? n : 0;
+}
+
+}  // namespace
+
+hipError_t launch_resident(const ResArgs& a, int rows, RuleKind rule, int grid, hipStream_t s)
+{
+    switch (rows) {
+    case 2: return launch_res_m<2>(a, rule, grid, s);
+    case 3: return launch_res_m<3>(a, rule, grid, s);
+    case 4: return launch_res_m<4>(a, rule, grid, s);
+    case 6: return launch_res_m<6>(a, rule, grid, s);
+    case 8: return launch_res_m<8>(a, rule, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+int resident_blocks_per_cu(int rows, RuleKind rule)
+{
+    switch (rows) {
+    case 2: return occupancy_res_m<2>(rule);
+    case 3: return occupancy_res_m<3>(rule);
+    case 4: return occupancy_res_m<4>(rule);
+    case 6: return occupancy_res_m<6>(rule);
+    case 8: return occupancy_res_m<8>(rule);
+    default: return 0;
+    }
+}
+
+}  // namespace gol

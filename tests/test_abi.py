@@ -62,7 +62,7 @@ def test_rank_rows_rejects_bad_args(pkg):
 
 def test_bad_config_rejected_before_touching_gpu(pkg):
     for kw in ({"rule": (512, 0)}, {"tb_depth": 3}, {"handoff": 3}, {"tb_depth": 20},
-               {"word_planes": 4}, {"handoff": 2, "tb_depth": 2}):
+               {"word_planes": 4}, {"handoff": 2, "tb_depth": 2}, {"resident": 3}):
         with pytest.raises(pkg.GolError) as ei:
             pkg.Engine(10, 10, **kw)
         assert ei.value.status == pkg.GOL_EINVAL
@@ -138,3 +138,6 @@ def test_shipped_library_has_only_product_kernels(pkg):
     assert depths == {1, 2, 4, 6, 7, 8, 12, 16}
     assert {int(n) for _, _, n, _ in names} == {2}
     assert {(int(k), int(h)) for k, _, _, h in names if int(h)} == {(k, 1) for k in (4, 6, 7, 8, 12, 16)}
+    # the resident kernel: 5 rows-per-wavefront variants x 3 rule kinds
+    res = set(re.findall(rb"life_res_kernelILi(\d)ELi(\d)E", blob))
+    assert res == {(str(m).encode(), str(r).encode()) for m in (2, 3, 4, 6, 8) for r in range(3)}

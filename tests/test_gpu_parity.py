@@ -276,17 +276,22 @@ def test_generic_rules(pkg, oracle, rule):
 
 # ------------------------------------------------------------ C2: 4096^2
 @pytest.mark.parametrize("rule", ["ref", "conway"])
-def test_c2_4096_per_generation(pkg, oracle, rule):
-    """The default C2 engine (K = 8): every checked generation count reached by one
+@pytest.mark.parametrize("kernel", ["resident", "streaming"])
+def test_c2_4096_per_generation(pkg, oracle, rule, kernel):
+    """The default C2 engine (the resident kernel, one launch per call) and the
+    streaming engine (K = 8): every checked generation count reached by one
     gol_step call from the initial field, so the depth-8 kernel and the remainder
-    depths run, plus gens 1..16 one call each for the early B/S2 generations."""
+    depths run (resident: partial and whole epochs), plus gens 1..16 one call
+    each for the early B/S2 generations."""
     h = w = 4096
     R = rules(oracle)[rule]
     g0 = oracle.bp_random(h, w, 1)
     want = {0: g0}
     for gen in range(1, 41):
         want[gen] = oracle.bp_run(want[gen - 1], w, 1, R, threads=16)
-    with pkg.Engine(h, w, rule=R, device=0) as e:
+    kw = {} if kernel == "resident" else {"resident": 1, "tb_depth": 8}
+    with pkg.Engine(h, w, rule=R, device=0, **kw) as e:
+        assert (e.resident is not None) == (kernel == "resident")
         e.init_random(1)
         assert (e.store_packed() == g0).all()
         for gens in (1, 2, 3, 5, 8, 9, 13, 16, 24, 40):

@@ -8,8 +8,8 @@
                          are known exactly (MI355X_MICROARCH.md §HBM):
                            digest_kernel      reads  rows*wq*8 B, 8 B per lane
                            init_random_kernel writes rows*stride*8 B, 8 B per lane
-  plus SQ_WAVE_CYCLES, SQ_WAIT_INST_ANY, GRBM_GUI_ACTIVE means and the effective
-  clock (GRBM_GUI_ACTIVE / 8 XCDs / mean kernel time from the kernel trace).
+  plus SQ_WAVE_CYCLES, SQ_WAIT_INST_ANY, GRBM_GUI_ACTIVE means, and the mean
+  launch time of the dominant stencil instantiation in the bench's kernel trace.
 
     python tools/pmc_counters.py gpurun_out/prof_r02a --out profiles/r02/counters.json
 """
@@ -78,13 +78,13 @@ def main():
         rec["insts_valu_per_launch"] = rec.get("sq_insts_valu_per_launch")
         rec["launches_profiled"] = len(per_kernel(sq, "SQ_INSTS_VALU").get("life_tb_kernel", []))
     stats = glob.glob(os.path.join(d, "trace", "*kernel_stats.csv"))
-    if stats:
-        for r in csv.DictReader(open(stats[0])):
-            if "life_tb_kernel" in r["Name"]:
-                rec["trace_avg_launch_ns"] = float(r["AverageNs"])
-                if rec.get("grbm_gui_active_per_launch"):
-                    rec["effective_clock_ghz"] = round(
-                        rec["grbm_gui_active_per_launch"] / 8 / float(r["AverageNs"]), 3)
+    if stats:  # the bench command's kernel trace: the dominant stencil instantiation
+        rows = [r for r in csv.DictReader(open(stats[0])) if "life_tb_kernel" in r["Name"]]
+        if rows:
+            top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+            rec["trace_kernel"] = top["Name"]
+            rec["trace_avg_launch_ns"] = float(top["AverageNs"])
+            rec["trace_calls"] = int(top["Calls"])
     rec["source"] = os.path.basename(os.path.normpath(d))
     doc = {"records": []}
     if os.path.exists(a.out):
