@@ -263,7 +263,7 @@ def main():
                 "rule": "B/S2 (reference effective rule)" if a.rule == "ref" else "B3/S23",
                 "tb_depth": eng.tb_depth, "word_planes": eng.word_planes,
                 "halo_depth": eng.halo_depth, "rows_per_wave": eng.rows_per_wave,
-                "handoff": eng.handoff,
+                "handoff": eng.handoff, "resident": eng.resident,
                 "parallelism": f"row-stripes x{world}" if world > 1 else "single GPU",
             },
             "roofline": {
@@ -274,7 +274,7 @@ def main():
                         "v_alignbit 2 slots)",
                 "frac": round(valu_achieved / peak_slot_rate, 4),
                 "traffic": traffic,
-                "kernel": "life_tb_kernel",
+                "kernel": "life_res_kernel" if eng.resident else "life_tb_kernel",
                 "avg_launch_ms": round(avg_launch_ms, 4),
                 "launches": tm["launches"],
                 "concurrent_streams": streams,

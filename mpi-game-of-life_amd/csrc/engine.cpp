@@ -752,10 +752,12 @@ gol_status timing_end(gol_engine* e, hipStream_t s, hipEvent_t e0, hipEvent_t e1
 // Resident plan: tiles of `band_rows` rows x one 64-lane strip, one 1024-thread
 // workgroup each (at most one per CU: every workgroup of the launch must be
 // resident at once, since tiles wait for their neighbours), each wavefront
-// holding `rows` rows, so a tile holds 16 rows x band + 2K halo rows.  Cost per
-// generation, in us: 0.03 + 0.025 rows (a workgroup barrier and 16 wavefronts
-// of rows + 2 H3 rows and rows rule rows on 4 SIMDs) + 2.0 / K (one flag
-// hand-off per epoch, MI355X_MICROARCH.md price list: handoff-flag).
+// holding `rows` rows, so a tile holds 16 rows >= band + 2K halo rows.  Cost per
+// generation, in us, fitted to 12 (rows, K, band) shapes at 4096^2
+// (profiles/r02/c2_resident_sweep.jsonl, within 8%): 0.17 + 0.046 (B + K) / 16
+// (the rows still exact, averaged over an epoch, per wavefront) + 0.068 rows
+// (barrier, LDS edge exchange, per-row fixed work) + 3.3 / K (the epoch hand-off:
+// publish, flag, neighbour wait, halo reload).
 gol_status plan_resident(gol_engine* e, const gol_config* cfg)
 {
     if (cfg->resident == 1 || e->nranks > 1 || e->sem != GOL_SEM_GLOBAL || e->planes != 2)
@@ -772,6 +774,8 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
     for (int M : gol::kResRowsList) {
         if (cfg->resident == 2 && cfg->rows_per_wave && (uint32_t)M != cfg->rows_per_wave) continue;
         if (gol::resident_blocks_per_cu(M, e->rule) < 1) continue;
+        // the generic-mask rule keeps 8 rows per wavefront only with spills
+        if (e->rule == gol::RULE_GENERIC && M > 6 && cfg->rows_per_wave != (uint32_t)M) continue;
         const int64_t NR = (int64_t)gol::kResWaves * M;
         const int64_t max_bands = std::min<int64_t>(cus / strips, h);
         for (int64_t nb = 1; nb <= max_bands; ++nb) {
@@ -783,7 +787,8 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
             if (K < 1 || K > kmax || (cfg->resident == 0 && K < 8)) continue;
             const int64_t span = (K + B - 1) / B;  // bands a K-row halo reaches
             if ((2 * span + 1) * (strips > 1 ? 3 : 1) - 1 > 64) continue;
-            const double cost = 0.03 + 0.025 * M + 2.0 / (double)K;
+            const double cost = 0.17 + 0.046 * (double)(B + K) / gol::kResWaves + 0.068 * M +
+                                3.3 / (double)K;
             if (cost < best * 0.999) {
                 best = cost;
                 e->res.rows = M;

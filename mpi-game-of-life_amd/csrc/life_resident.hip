@@ -15,11 +15,13 @@
 // streaming kernel does).  One 1024-thread workgroup per (band, strip), at most
 // one per CU: its 16 wavefronts hold M consecutive rows each in VGPRs, rows
 // [b0 - K, b0 - K + 16 M) ⊇ [b0 - K, b1 + K), the band plus K halo rows on each
-// side.  A generation is: every wavefront puts its first and last row in LDS,
-// one workgroup barrier, it reads the row above its first and below its last,
-// and computes its M rows in registers.  Rows at the edge of the held range are
-// wrong by one more row per generation, so after K generations exactly the
-// band is valid: an epoch.
+// side.  A generation is: every wavefront forms the H3 sums (bit-sliced
+// horizontal 3-cell sums) of its M rows, puts those of its first and last row in
+// LDS, one workgroup barrier, it reads the H3 of the row above its first and
+// below its last, and computes its M rows in registers.  Rows at the edge of the
+// held range are wrong by one more row per generation, so after K generations
+// exactly the band is valid: an epoch.  Waves whose rows are all already
+// outside the shrinking exact range skip the work.
 //
 // Between epochs (every K generations) a workgroup publishes its band rows to
 // the ping-pong field buffer of the next epoch (write-through sc1 stores), then
@@ -43,7 +45,7 @@ namespace gol {
 namespace {
 
 constexpr int kResLdsWords = 96 * 1024 / 8;  // > 80 KB: one workgroup per CU
-static_assert(2 * 2 * kResWaves * 64 <= kResLdsWords, "edge rows fit the LDS block");
+static_assert(2 * 2 * kResWaves * 64 * 2 <= kResLdsWords, "edge H3 rows fit the LDS block");
 
 // H3 of a row: bit-sliced sum (s) and carry (c) of each cell and its 2
 // horizontal neighbours (life_stencil.h stage_step's first half).
@@ -136,34 +138,77 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
         }
     }
 
+    // H3 (bit-sliced horizontal 3-sums) of this wave's rows, kept across steps so
+    // that a wave that skips a generation still publishes defined values
+    Pl<2> s[M], c[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) s[i] = c[i] = zero_pl();
+    uint4* const ed4 = reinterpret_cast<uint4*>(lds);
+
     uint32_t epoch = 0;
     bool gave_up = false;
+    // edge H3 rows through LDS: slot p = [top/bottom][wave][lane], 2 slots
+    auto put_edges = [&](int p) {
+        if constexpr (!(GOL_EXP & 32)) {
+            uint4* ed = ed4 + p * (2 * W * 64);
+            ed[wv * 64 + lane] = uint4{s[0].v[0], s[0].v[1], c[0].v[0], c[0].v[1]};
+            ed[(W + wv) * 64 + lane] = uint4{s[M - 1].v[0], s[M - 1].v[1], c[M - 1].v[0],
+                                             c[M - 1].v[1]};
+        }
+    };
+    auto rule_row = [&](int i, const Pl<2>& as, const Pl<2>& ac, const Pl<2>& es,
+                        const Pl<2>& ec) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            uint32_t y = rule32_total<RULE>(as.v[q], ac.v[q], s[i].v[q], c[i].v[q], es.v[q],
+                                            ec.v[q], x[i].v[q], a.birth, a.survive);
+            if constexpr (kBirths) y = lop3<kAnd3>(y, cm.v[q], rowm[i]);
+            x[i].v[q] = y;
+        }
+    };
     for (int32_t done = 0; done < a.gens;) {
         const int32_t k = min(a.K, a.gens - done);
+#pragma unroll
+        for (int i = 0; i < M; ++i) h3_row(x[i], s[i], c[i]);
+        put_edges(0);
         for (int32_t g = 0; g < k; ++g) {
-            uint64_t* ed = lds + (g & 1) * (2 * W * 64);  // [top/bottom][wave][lane]
-            Pl<2> up = zero_pl(), dn = zero_pl();
+            // after generation g+1 of the epoch only rows [lo, hi) of the held range
+            // are exact: a wave with none of them skips the work (the rows its
+            // neighbours would compute from it are discarded), and the H3 of the
+            // next generation is needed exactly for the rows this one computes
+            const int64_t lo = b0 - a.K + g + 1, hi = b1 + a.K - g - 1;
+            const bool on = r0 + M > lo && r0 < hi;
+            if constexpr (!(GOL_EXP & 16)) __syncthreads();
+            Pl<2> us = zero_pl(), uc = zero_pl(), ds = zero_pl(), dc = zero_pl();
             if constexpr (!(GOL_EXP & 32)) {
-                ed[wv * 64 + lane] = words_of<2>(x[0]).w[0];
-                ed[(W + wv) * 64 + lane] = words_of<2>(x[M - 1]).w[0];
-                if constexpr (!(GOL_EXP & 16)) __syncthreads();
-                if (wv > 0) up = planes_of<2>(Grp<2>{{ed[(W + wv - 1) * 64 + lane]}});
-                if (wv < W - 1) dn = planes_of<2>(Grp<2>{{ed[(wv + 1) * 64 + lane]}});
+                const uint4* ed = ed4 + (g & 1) * (2 * W * 64);
+                if (wv > 0) {
+                    const uint4 t = ed[(W + wv - 1) * 64 + lane];
+                    us.v[0] = t.x; us.v[1] = t.y; uc.v[0] = t.z; uc.v[1] = t.w;
+                }
+                if (wv < W - 1) {
+                    const uint4 t = ed[(wv + 1) * 64 + lane];
+                    ds.v[0] = t.x; ds.v[1] = t.y; dc.v[0] = t.z; dc.v[1] = t.w;
+                }
             }
-            Pl<2> s[M + 2], c[M + 2];
-            h3_row(up, s[0], c[0]);
+            if (on) {
+                // interior rows first (no LDS operand: they cover the LDS read),
+                // then the edge rows; next generation's H3: edges first, so their
+                // LDS write is covered by the interior H3 and the barrier
 #pragma unroll
-            for (int i = 0; i < M; ++i) h3_row(x[i], s[i + 1], c[i + 1]);
-            h3_row(dn, s[M + 1], c[M + 1]);
+                for (int i = 1; i < M - 1; ++i) rule_row(i, s[i - 1], c[i - 1], s[i + 1], c[i + 1]);
+                if constexpr (M == 1) {
+                    rule_row(0, us, uc, ds, dc);
+                } else {
+                    rule_row(0, us, uc, s[1], c[1]);
+                    rule_row(M - 1, s[M - 2], c[M - 2], ds, dc);
+                }
+                if (g + 1 < k) {
+                    h3_row(x[0], s[0], c[0]);
+                    if constexpr (M > 1) h3_row(x[M - 1], s[M - 1], c[M - 1]);
+                    put_edges((g + 1) & 1);
 #pragma unroll
-            for (int i = 0; i < M; ++i) {
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    uint32_t y = rule32_total<RULE>(s[i].v[q], c[i].v[q], s[i + 1].v[q], c[i + 1].v[q],
-                                                    s[i + 2].v[q], c[i + 2].v[q], x[i].v[q], a.birth,
-                                                    a.survive);
-                    if constexpr (kBirths) y = lop3<kAnd3>(y, cm.v[q], rowm[i]);
-                    x[i].v[q] = y;
+                    for (int i = 1; i < M - 1; ++i) h3_row(x[i], s[i], c[i]);
                 }
             }
         }
