@@ -174,10 +174,12 @@ gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_pe
 
 /* Whether full-depth launches use hand-off row blocks (gol_config.handoff, as
  * the planner resolved it): 1 = yes, 0 = every block recomputes its halo. */
-/* Resident plan (gol_config.resident): *on = 1 if gol_step runs the resident
- * kernel; then *bands x *strips tiles, one workgroup each. */
-gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint32_t* strips);
 gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff);
+
+/* Resident plan (gol_config.resident): *on = 1 if gol_step runs the resident
+ * kernel; then *bands x *strips tiles, one workgroup each (bands, strips may be
+ * NULL).  A composite engine reports 0. */
+gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint32_t* strips);
 
 /* ---- Multi-GPU, one process per GPU (replaces the MPI stripes :70-81 and the
  * halo exchange :104-145 with RCCL send/recv over xGMI) ---- */

@@ -1,8 +1,8 @@
 """GPU parity at the benchmark sizes (BASELINE.json configs[2..4]).
 
 The timed path itself: gol_create(65536, 65536) with defaults is the composite
-engine (2 same-device stripes on 2 streams, 256-row halo rounds, K = 16, hand-off
-row blocks) -- exactly what bench.py measures.  Checked
+engine (2 same-device stripes on 2 streams, 256-row halo rounds, K = 16, row
+blocks as the planner picks them) -- exactly what bench.py measures.  Checked
   * against the CPU oracle after one step(16) call (the K = 16 kernel runs);
   * after 600 more generations (two overlapped 256-generation rounds and a
     partial one) against a streams=1, tb_depth=1, classic-block engine, which the
@@ -32,7 +32,7 @@ def digest_of(pkg, h, w, rule, gens, seed=1, **kw):
 def test_c3_default_engine_vs_oracle_and_depth1(pkg, oracle, rule):
     R = oracle.REF_RULE if rule == "ref" else oracle.CONWAY
     with pkg.Engine(N, N, rule=R, device=0) as e:
-        assert e.tb_depth == 16 and e.handoff, (e.tb_depth, e.handoff)
+        assert e.tb_depth == 16 and e.resident is None, (e.tb_depth, e.resident)
         e.init_random(1)
         e.step(16)  # one full-depth launch per stripe
         d16 = e.digest()
