@@ -31,6 +31,8 @@ thread_local std::string g_last_error;
 // stripes on 2 streams (measured +11% at 65536^2; no gain at <= 16384 rows,
 // profiles/r01/group_bench_*.jsonl)
 constexpr uint64_t kCompositeMinRows = 32768;
+// hand-off flag buffers start with a ticket counter on its own 256-byte line
+constexpr int64_t kTicketWords = 64;
 // captured step graphs kept per engine (least recently used evicted)
 constexpr size_t kGraphCache = 8;
 
@@ -300,10 +302,11 @@ bool handoff_fits(int64_t R, int d, int planes) { return gol::handoff_toff(R, d,
 // resident ones, and a partial round of m wavefronts still costs max(2, m) issue
 // slots per instruction (one wavefront alone issues at half the SIMD's VALU rate).
 // A wavefront's time in rows of K stage-steps: classic blocks R + K + 1 (+ c0
-// fixed); hand-off blocks skip the K - 1 rows of vertical halo but their steady
-// loop runs ~4% slower per row (bigger code, side-row refills):
-// 1.04 R + 12, fitted to the in-process A/B of profiles/r02/ab_handoff_shapes.jsonl
-// (8448 rows: hand-off 5% faster; 33024 / 65536 rows: classic 1-4% faster).  Measured
+// fixed); hand-off blocks skip the K - 1 rows of vertical halo, pay their signal,
+// wait and side-row blocks: 1.02 R + 10, fitted at K = 16 to the in-process A/B
+// of profiles/r02/ab_handoff_hybrid.jsonl (hand-off 9% faster at 8448 rows, 5% at
+// 16640, 1% at 33024 and 65536 -- the hot loop is the classic one since the
+// side-row refills were peeled off it).  Measured
 // (profiles/r01/sweep_rows_per_wave*.jsonl): keeping fewer than `occ`
 // wavefronts per SIMD all launch long is 5-10% slower than the model says, so R
 // is restricted to n >= occ whenever the field is large enough.  Narrower strips
@@ -348,7 +351,7 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
                 const int64_t full = n / occ, rem = n % occ;
                 const double slots =
                     (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
-                const double rows = hand ? 1.04 * (double)R + 12.0 : (double)(R + K + 1 + c0);
+                const double rows = hand ? 1.02 * (double)R + 10.0 : (double)(R + K + 1 + c0);
                 const double cost = slots * rows;
                 const int filled = n >= occ ? 1 : 0;
                 if (cost < best[hand][filled] * 0.999) {
@@ -382,6 +385,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     // (all launches of a step then share one kernel kind; a plan where hand-off
     // does not fit still falls back to classic blocks)
     uint32_t handoff = e->handoff;
+    if (!gol::handoff_kernel_exists((int)e->K, e->rule)) handoff = 1;
     if (handoff == 0 && !raw.empty())
         handoff = pick_rows_per_wave(raw[0], e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
                                      (int)e->rows_per_wave, e->lane_shift, 0)
@@ -432,8 +436,9 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         const int regions = e->overlap ? 2 : 1;
         for (int r = 0; r < regions; ++r) {
             HIP_TRY(hipMalloc(&e->side[r], (size_t)max_units * slot * sizeof(uint64_t)));
-            HIP_TRY(hipMalloc(&e->flags[r], (size_t)max_units * sizeof(uint32_t)));
-            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)max_units * sizeof(uint32_t)));
+            // word 0: the launch's ticket counter; its own 256-byte line, then the flags
+            HIP_TRY(hipMalloc(&e->flags[r], (size_t)(max_units + kTicketWords) * sizeof(uint32_t)));
+            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)(max_units + kTicketWords) * sizeof(uint32_t)));
         }
     }
     return GOL_OK;
@@ -873,10 +878,12 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     a.birth = e->birth;
     a.survive = e->survive;
     const bool hand = p.hand && p.multi_blk && e->side[region] &&
-                      handoff_fits(p.rpw, (int)depth, e->planes);
+                      handoff_fits(p.rpw, (int)depth, e->planes) &&
+                      gol::handoff_kernel_exists((int)depth, e->rule);
     if (hand) {
         a.side = e->side[region];
-        a.flags = e->flags[region];
+        a.flags = e->flags[region] + kTicketWords;
+        a.ticket = e->flags[region];
         a.err = e->d_err;
         a.side_slot = (int64_t)2 * (depth - 1) * 64 * (e->planes / 2);
         a.tail_off = gol::handoff_toff(p.rpw, (int)depth, e->planes);
@@ -947,7 +954,7 @@ gol_status check_err(gol_engine* e)
                 for (const auto& p : e->plans) m = std::max(m, p.total_units);
                 return m;
             }();
-            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)n * sizeof(uint32_t)));
+            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)(n + kTicketWords) * sizeof(uint32_t)));
         }
     return fail(GOL_EHIP, "a wait for a neighbour's rows timed out in the stencil kernel; "
                           "the field is not valid");

@@ -67,6 +67,7 @@ struct StepArgs {
     // flag the kernel sets when a wait for a neighbour's rows timed out.
     uint64_t* side;       // total_units slots of side_slot words
     uint32_t* flags;      // total_units words, all 0 between launches
+    uint32_t* ticket;     // 0 between launches: hands out work units in start order
     int* err;
     int64_t side_slot;    // words per slot: 2 (K-1) rows x 64 lanes x NP/2 words
 };
@@ -84,6 +85,12 @@ constexpr bool kDevKernels = GOL_DEV_KERNELS != 0;
 // Row blocks hand their first rows of every fused generation to the block above
 // (life_stencil.h) from this depth on.
 constexpr int kHandoffMinDepth = 4;
+// ... except for the generic-mask rule above depth 12, whose 10-term mask sum
+// already spills without the hand-off's extra state (auto_layout gives it K = 12)
+constexpr bool handoff_kernel_exists(int K, RuleKind rule)
+{
+    return K >= kHandoffMinDepth && (rule != RULE_GENERIC || K <= 12);
+}
 
 // Steps per block of the stencil kernel's register prefetch ring (host copy of
 // life_stencil.h kPfOf): 8 for 2-plane kernels of depth >= 16, 4 elsewhere.

@@ -39,9 +39,10 @@
 //     block below, which computed them first thing (its first two rows of every
 //     generation).  Each block writes those 2(K-1) "side rows" to its slot,
 //     signals a flag, and the block above reads them at the end of its stream:
-//     stage s computes exactly R + 2 rows.  Blocks are numbered bottom-up, so a
-//     block's producer always has the smaller wavefront index (dispatched no
-//     later); waits are bounded and a timeout sets *err instead of hanging.
+//     stage s computes exactly R + 2 rows.  Blocks are numbered bottom-up and
+//     units are drawn from a ticket counter in start order (see the kernel), so a
+//     block's producer has always started before it; waits are bounded and a
+//     timeout sets *err instead of hanging.
 //     Hand-off memory protocol (MI355X_MICROARCH.md, inter-workgroup
 //     visibility, first table row): side rows stored write-through (sc1), the
 //     producer's s_waitcnt vmcnt(0), an sc1 flag store by one lane; the consumer
@@ -300,6 +301,9 @@ __device__ __forceinline__ void place_block(Pl<NP> (&x)[PF])
 // so that the launch always drains.
 constexpr int kPollLimit = 1 << 16;
 
+// Block modes of the stencil kernel (see `block`).
+constexpr int kWarmBlk = 0, kPure = 1, kSide = 2;
+
 // Dev timing experiments only (tools/exp_build.sh; results are NOT valid): bit 0
 // skips the consumer's wait, bit 1 the producer's drain + flag, bit 2 the
 // side-row stores, bit 3 the consumer's tail.
@@ -319,8 +323,26 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     static_assert(!HAND || K >= kHandoffMinDepth, "hand-off kernels start at kHandoffMinDepth");
     static_assert(TOFF >= 0 && TOFF < kPrefetch && (HAND || TOFF == 0), "tail offset");
     const int lane = threadIdx.x & 63;
-    const int64_t unit =
-        (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int64_t unit;
+    if constexpr (HAND) {
+        // Hand-off kernels take their unit from a ticket counter, so a wave's unit
+        // index is its start order: the producer a consumer waits for has always
+        // started (is resident) and signals before it waits itself.  Block index
+        // order is not start order -- HIP promises none, each XCD dispatches its
+        // own blocks, and a concurrent launch on another stream (composite
+        // stripes, band + interior) can hold one XCD's slots -- and two hand-off
+        // launches side by side could otherwise wait on each other until the
+        // poll limit.  The wave that draws the last ticket resets the counter.
+        uint32_t t = 0;
+        if (lane == 0)
+            t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t == gridDim.x * kWavesPerBlock - 1 && lane == 0)
+            __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unit = t;
+    } else {
+        unit = (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    }
     if (unit >= a.total_units) return;
 
     int sidx = 0;
@@ -406,13 +428,17 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     for (int p = 0; p < kPrefetch; ++p) ring[p] = load_step(p);
 
     // row of step t: an input row is dead outside the field / buffer; a side row
-    // comes as the block below computed it; columns >= w masked
-    auto ingest = [&](int32_t t, const Grp<NP>& xv) -> Pl<NP> {
-        const bool ok = (HAND && t >= t_side) || ((t >= t_lo) && (t < t_hi));
+    // comes as the block below computed it; columns >= w masked.  SIDE: the step
+    // may be a side row (a consumer's last blocks); else it is an input row.
+    auto ingest = [&](int32_t t, const Grp<NP>& xv, auto side) -> Pl<NP> {
+        const bool ok = (decltype(side)::value && t >= t_side) || ((t >= t_lo) && (t < t_hi));
         Pl<NP> x = planes_of(xv);
 #pragma unroll
         for (int k = 0; k < NP; ++k) x.v[k] = ok ? (x.v[k] & cm.v[k]) : 0u;
         return x;
+    };
+    auto load_in = [&](int32_t s) -> Grp<NP> {
+        return load_grp<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
     };
     // stage g (generation g+1) at step t: emits local row row_first + t - (g+1)
     auto stage = [&](int g, int32_t t, Pl<NP> x) -> Pl<NP> {
@@ -468,19 +494,31 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
             wait_below();
     };
 
-    // One block of kPrefetch steps from step t0.  GUARD (warm-up blocks): stage g
-    // first emits a row that can reach a valid output at step 2g+2 and needs the
-    // two ingests before it, so it only runs from step 2g on; skipping it earlier
-    // saves K*(K-1) of the 2K*K warm-up stage-steps.  In the warm-up blocks of a
-    // hand-off kernel, stage g's outputs at steps 2g+2 and 2g+3 (its first two rows,
-    // generation g+1) are also stored as side rows 2g and 2g+1 for the block above.
-    auto block = [&](int32_t t0, auto guard) {
-        constexpr bool kGuard = decltype(guard)::value;
+    // One block of kPrefetch steps from step t0, in one of four modes:
+    //  * kWarmBlk (warm-up blocks): stage g first emits a row that can reach a valid
+    //    output at step 2g+2 and needs the two ingests before it, so it only runs
+    //    from step 2g on; skipping it earlier saves K*(K-1) of the 2K*K warm-up
+    //    stage-steps.  In the warm-up blocks of a hand-off kernel, stage g's outputs
+    //    at steps 2g+2 and 2g+3 (its first two rows, generation g+1) are also stored
+    //    as side rows 2g and 2g+1 for the block above;
+    //  * kPure: the steady-state loop -- input rows only (a hand-off kernel's
+    //    signal and wait are scalar-guarded calls in it);
+    //  * kSide (hand-off consumers): the last 1-2 steady blocks, whose refill may
+    //    reach the side rows (a per-load select).  Peeling them keeps the selects out
+    //    of the hot loop; a third copy for the first steady block cost more in
+    //    instruction cache than it saved (profiles/r02/ab_handoff_peeled.jsonl).
+    auto block = [&](int32_t t0, auto mode) {
+        constexpr int kMode = decltype(mode)::value;
+        constexpr bool kGuard = kMode == kWarmBlk;
+        constexpr bool kSideMode = HAND && kMode == kSide;
         Pl<NP> x[kPrefetch];
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
-            x[p] = ingest(t0 + p, ring[p]);
-            ring[p] = load_step(t0 + kPrefetch + p);
+            x[p] = ingest(t0 + p, ring[p], std::integral_constant<bool, kSideMode>{});
+            if constexpr (kSideMode)
+                ring[p] = load_step(t0 + kPrefetch + p);
+            else
+                ring[p] = load_in(t0 + kPrefetch + p);
         }
         // Code placement (steady-state blocks).  gfx950 issues this kernel's
         // instruction mix (DPP move, v_alignbit, v_bitop3 chains; all 8-byte
@@ -531,13 +569,21 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     constexpr int kWarm = kWarmSteps;
     static_assert(!HAND || kWarm >= 2 * K, "side rows are all stored in the warm-up blocks");
 #pragma unroll
-    for (int t0 = 0; t0 < kWarm; t0 += kPrefetch) block(t0, std::true_type{});
+    for (int t0 = 0; t0 < kWarm; t0 += kPrefetch) block(t0, std::integral_constant<int, kWarmBlk>{});
 
     // Steady state: whole blocks of input steps.  A consumer stops TOFF steps
     // before t_side; its last whole block's refill is the first to reach t_side.
+    // The hand-off kernel's first block and a consumer's last blocks (whose
+    // refills reach the side rows) are peeled off the hot loop.
     int32_t t0 = kWarm;
-    for (; consumer ? t0 + kPrefetch + TOFF <= t_side : t0 < T; t0 += kPrefetch)
-        block(t0, std::false_type{});
+    if constexpr (!HAND) {
+        for (; t0 < T; t0 += kPrefetch) block(t0, std::integral_constant<int, kPure>{});
+    } else {
+        auto more = [&](int32_t t) { return consumer ? t + kPrefetch + TOFF <= t_side : t < T; };
+        for (; consumer ? t0 + 2 * kPrefetch + TOFF <= t_side : t0 < T; t0 += kPrefetch)
+            block(t0, std::integral_constant<int, kPure>{});
+        for (; more(t0); t0 += kPrefetch) block(t0, std::integral_constant<int, kSide>{});
+    }
     // a producer whose stream had no steady block (a short last block) signals here
     if constexpr (HAND)
         if (producer && T <= kWarm && !(GOL_EXP & 2)) signal();
@@ -550,7 +596,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
             if constexpr (TOFF > 0) {
                 Pl<NP> x[TOFF];
 #pragma unroll
-                for (int p = 0; p < TOFF; ++p) x[p] = ingest(t0 + p, ring[p]);
+                for (int p = 0; p < TOFF; ++p) x[p] = ingest(t0 + p, ring[p], std::true_type{});
 #pragma unroll
                 for (int p = 0; p + TOFF < kPrefetch; ++p) ring[p] = ring[p + TOFF];
 #pragma unroll
@@ -575,7 +621,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
                 Pl<NP> x[kPrefetch];
 #pragma unroll
                 for (int p = 0; p < kPrefetch; ++p) {
-                    x[p] = ingest(tb + tau0 + p, ring[p]);
+                    x[p] = ingest(tb + tau0 + p, ring[p], std::true_type{});
                     if (tau0 + kPrefetch + p < kSideRows)
                         ring[p] = load_step(tb + tau0 + kPrefetch + p);
                 }
@@ -613,7 +659,10 @@ hipError_t launch_kernel(const StepArgs& a, RuleKind rule, hipStream_t s)
         hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, NP, HAND, TOFF>), grid, block, 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, NP, HAND, TOFF>), grid, block, 0, s, a);
+        if constexpr (!HAND || handoff_kernel_exists(K, RULE_GENERIC))
+            hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, NP, HAND, TOFF>), grid, block, 0, s, a);
+        else
+            return hipErrorInvalidValue;
         break;
     }
     return hipGetLastError();
@@ -631,7 +680,7 @@ int occupancy_kernel(RuleKind rule)
     else if (rule == RULE_CONWAY)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &blocks, life_tb_kernel<K, RULE_CONWAY, NP, HAND, TOFF>, threads, 0);
-    else
+    else if constexpr (!HAND || handoff_kernel_exists(K, RULE_GENERIC))
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &blocks, life_tb_kernel<K, RULE_GENERIC, NP, HAND, TOFF>, threads, 0);
     return e == hipSuccess ? blocks : 0;

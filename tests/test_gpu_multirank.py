@@ -177,3 +177,40 @@ def test_group_reload_one_member(pkg, oracle):
         m.load_packed(mid[m.row0:m.row0 + m.rows])  # same rows, halos now stale
         grp.step(48)
         assert (grp.store_packed() == oracle.bp_run(mid, w, 48, oracle.CONWAY)).all()
+
+
+def test_concurrent_handoff_launches(pkg):
+    """Hand-off launches on several streams at once (two engines plus a
+    composite): consumers only ever wait for producers that have started, so no
+    launch can hold the slots another launch's producers need (ticket order, not
+    block order).  Results equal the same engines stepped one at a time, and no
+    wait times out."""
+    shapes = [(6144, 16384), (5000, 12000)]
+    gens = [160, 97]
+    want = []
+    for (h, w), g in zip(shapes, gens):
+        with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, tb_depth=16, handoff=2, streams=1,
+                        resident=1) as e:
+            e.init_random(h)
+            e.step(g)
+            want.append(e.digest())
+    with pkg.Engine(32768, 8192, rule=pkg.CONWAY, device=0, handoff=2) as c:
+        c.init_random(3)
+        engines = [pkg.Engine(h, w, rule=pkg.CONWAY, device=0, tb_depth=16, handoff=2,
+                              streams=1, resident=1) for h, w in shapes]
+        try:
+            for rep in range(3):
+                for e, (h, w) in zip(engines, shapes):
+                    assert e.handoff
+                    e.init_random(h)
+                # interleave: every engine's launches queued before any sync
+                for k in range(4):
+                    c.step(40)
+                    for e, g in zip(engines, gens):
+                        e.step(g // 4 if k < 3 else g - 3 * (g // 4))
+                for e, d in zip(engines, want):
+                    assert e.digest() == d, f"repetition {rep}"
+                c.sync()
+        finally:
+            for e in engines:
+                e.close()
