@@ -31,8 +31,6 @@ thread_local std::string g_last_error;
 // stripes on 2 streams (measured +11% at 65536^2; no gain at <= 16384 rows,
 // profiles/r01/group_bench_*.jsonl)
 constexpr uint64_t kCompositeMinRows = 32768;
-// hand-off flag buffers start with a ticket counter on its own 256-byte line
-constexpr int64_t kTicketWords = 64;
 // captured step graphs kept per engine (least recently used evicted)
 constexpr size_t kGraphCache = 8;
 
@@ -396,8 +394,12 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         const auto& r = raw[pi];
         gol_engine::Plan p;
         p.segs = r;
+        // the band launch runs beside the interior launch: classic blocks, so that
+        // at most one launch that waits for its own wavefronts runs at a time
+        const bool band = e->overlap && pi == (size_t)e->Hx;
         const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
-                                              (int)e->rows_per_wave, e->lane_shift, handoff);
+                                              (int)e->rows_per_wave, e->lane_shift,
+                                              band ? 1u : handoff);
         p.rpw = rp.rpw;
         p.groups = rp.groups;
         p.lane_shift = rp.lane_shift;
@@ -436,9 +438,8 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         const int regions = e->overlap ? 2 : 1;
         for (int r = 0; r < regions; ++r) {
             HIP_TRY(hipMalloc(&e->side[r], (size_t)max_units * slot * sizeof(uint64_t)));
-            // word 0: the launch's ticket counter; its own 256-byte line, then the flags
-            HIP_TRY(hipMalloc(&e->flags[r], (size_t)(max_units + kTicketWords) * sizeof(uint32_t)));
-            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)(max_units + kTicketWords) * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&e->flags[r], (size_t)max_units * sizeof(uint32_t)));
+            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)max_units * sizeof(uint32_t)));
         }
     }
     return GOL_OK;
@@ -882,8 +883,7 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
                       gol::handoff_kernel_exists((int)depth, e->rule);
     if (hand) {
         a.side = e->side[region];
-        a.flags = e->flags[region] + kTicketWords;
-        a.ticket = e->flags[region];
+        a.flags = e->flags[region];
         a.err = e->d_err;
         a.side_slot = (int64_t)2 * (depth - 1) * 64 * (e->planes / 2);
         a.tail_off = gol::handoff_toff(p.rpw, (int)depth, e->planes);
@@ -954,7 +954,7 @@ gol_status check_err(gol_engine* e)
                 for (const auto& p : e->plans) m = std::max(m, p.total_units);
                 return m;
             }();
-            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)(n + kTicketWords) * sizeof(uint32_t)));
+            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)n * sizeof(uint32_t)));
         }
     return fail(GOL_EHIP, "a wait for a neighbour's rows timed out in the stencil kernel; "
                           "the field is not valid");
@@ -1038,6 +1038,10 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
         // composite: S same-device stripes with deep halos, advanced together
         gol_config c = *cfg;
         c.streams = 1;
+        // the stripes run side by side on one device, so at most one of them could
+        // keep hand-off blocks (gol_create_group); unbalanced stripes lose more than
+        // that one gains (profiles/r02/ab_handoff_policy.jsonl): classic blocks
+        if (c.handoff == 0) c.handoff = 1;
         const Layout lay = auto_layout(h / S, cfg);
         c.tb_depth = lay.K;
         c.word_planes = (uint32_t)lay.planes;
@@ -1240,9 +1244,19 @@ gol_status gol_create_group(uint64_t h, uint64_t w, const gol_config* cfg, int n
     if (!engines || nranks <= 0) return fail(GOL_EINVAL, "bad group arguments");
     for (int r = 0; r < nranks; ++r) engines[r] = nullptr;
     gol_status st = GOL_OK;
+    // Hand-off row blocks wait for other wavefronts of their own launch, which
+    // is safe when only one such launch runs on a device at a time (a launch's
+    // blocks start in order on each XCD; two waiting launches side by side could
+    // hold each other's slots).  Members sharing a device run concurrently, so
+    // only the first member on each device keeps hand-off blocks.
+    std::vector<int> devs;
     for (int r = 0; r < nranks && st == GOL_OK; ++r) {
         gol_config c = *cfg;
         c.device = devices ? devices[r] : (cfg->device >= 0 ? cfg->device : -1);
+        int d = c.device;
+        if (d < 0 && hipGetDevice(&d) != hipSuccess) d = -1;
+        if (std::find(devs.begin(), devs.end(), d) != devs.end()) c.handoff = 1;
+        devs.push_back(d);
         st = make_rank_engine(h, w, &c, r, nranks, &engines[r]);
     }
     for (int r = 0; r < nranks && st == GOL_OK; ++r) {

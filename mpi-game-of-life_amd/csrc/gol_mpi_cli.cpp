@@ -182,6 +182,19 @@ int main(int argc, char** argv)
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail_all(rank, "no HIP device");
     cfg.device = local_rank(rank) % ndev;
+    {
+        // more ranks on this node than devices: ranks share GPUs, and hand-off row
+        // blocks are kept to one launch per device at a time (engine.cpp
+        // gol_create_group), so ranks that share one use classic blocks
+        MPI_Comm node;
+        int node_size = 1;
+        if (MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node) ==
+            MPI_SUCCESS) {
+            MPI_Comm_size(node, &node_size);
+            MPI_Comm_free(&node);
+        }
+        if (node_size > ndev) cfg.handoff = 1;
+    }
 
     uint8_t uid[128] = {};
     if (transport == "rccl") {

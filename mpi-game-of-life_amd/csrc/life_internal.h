@@ -66,8 +66,7 @@ struct StepArgs {
     // life_stencil.h): each wavefront's slot of side rows, its ready flag, and a
     // flag the kernel sets when a wait for a neighbour's rows timed out.
     uint64_t* side;       // total_units slots of side_slot words
-    uint32_t* flags;      // total_units words, all 0 between launches
-    uint32_t* ticket;     // 0 between launches: hands out work units in start order
+    uint32_t* flags;      // total_units words, zeroed before every launch
     int* err;
     int64_t side_slot;    // words per slot: 2 (K-1) rows x 64 lanes x NP/2 words
 };

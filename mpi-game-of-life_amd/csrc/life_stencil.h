@@ -39,10 +39,14 @@
 //     block below, which computed them first thing (its first two rows of every
 //     generation).  Each block writes those 2(K-1) "side rows" to its slot,
 //     signals a flag, and the block above reads them at the end of its stream:
-//     stage s computes exactly R + 2 rows.  Blocks are numbered bottom-up and
-//     units are drawn from a ticket counter in start order (see the kernel), so a
-//     block's producer has always started before it; waits are bounded and a
-//     timeout sets *err instead of hanging.
+//     stage s computes exactly R + 2 rows.  Blocks are numbered bottom-up: each
+//     XCD starts its share of a launch's blocks in order, so the block a waiting
+//     consumer depends on has a smaller index and cannot be queued behind waiting
+//     blocks of the same launch.  A second launch that waits could hold an XCD's
+//     slots, so the engine runs at most one hand-off launch per device at a time
+//     (engine.cpp: band launches and group members after the first on a device
+//     use classic blocks).  Waits are bounded; a timeout sets *err (reported by
+//     gol_sync) instead of hanging.
 //     Hand-off memory protocol (MI355X_MICROARCH.md, inter-workgroup
 //     visibility, first table row): side rows stored write-through (sc1), the
 //     producer's s_waitcnt vmcnt(0), an sc1 flag store by one lane; the consumer
@@ -323,26 +327,8 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     static_assert(!HAND || K >= kHandoffMinDepth, "hand-off kernels start at kHandoffMinDepth");
     static_assert(TOFF >= 0 && TOFF < kPrefetch && (HAND || TOFF == 0), "tail offset");
     const int lane = threadIdx.x & 63;
-    int64_t unit;
-    if constexpr (HAND) {
-        // Hand-off kernels take their unit from a ticket counter, so a wave's unit
-        // index is its start order: the producer a consumer waits for has always
-        // started (is resident) and signals before it waits itself.  Block index
-        // order is not start order -- HIP promises none, each XCD dispatches its
-        // own blocks, and a concurrent launch on another stream (composite
-        // stripes, band + interior) can hold one XCD's slots -- and two hand-off
-        // launches side by side could otherwise wait on each other until the
-        // poll limit.  The wave that draws the last ticket resets the counter.
-        uint32_t t = 0;
-        if (lane == 0)
-            t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = __builtin_amdgcn_readfirstlane(t);
-        if (t == gridDim.x * kWavesPerBlock - 1 && lane == 0)
-            __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unit = t;
-    } else {
-        unit = (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    }
+    const int64_t unit =
+        (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (unit >= a.total_units) return;
 
     int sidx = 0;
@@ -504,8 +490,8 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     //  * kPure: the steady-state loop -- input rows only (a hand-off kernel's
     //    signal and wait are scalar-guarded calls in it);
     //  * kSide (hand-off consumers): the last 1-2 steady blocks, whose refill may
-    //    reach the side rows (a per-load select).  Peeling them keeps the selects out
-    //    of the hot loop; a third copy for the first steady block cost more in
+    //    reach the side rows (a per-load select).  Peeling them keeps the selects
+    //    out of the hot loop; a third copy for the first steady block cost more in
     //    instruction cache than it saved (profiles/r02/ab_handoff_peeled.jsonl).
     auto block = [&](int32_t t0, auto mode) {
         constexpr int kMode = decltype(mode)::value;
@@ -579,10 +565,12 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     if constexpr (!HAND) {
         for (; t0 < T; t0 += kPrefetch) block(t0, std::integral_constant<int, kPure>{});
     } else {
-        auto more = [&](int32_t t) { return consumer ? t + kPrefetch + TOFF <= t_side : t < T; };
+        // the consumer's wait is in the last pure block
         for (; consumer ? t0 + 2 * kPrefetch + TOFF <= t_side : t0 < T; t0 += kPrefetch)
             block(t0, std::integral_constant<int, kPure>{});
-        for (; more(t0); t0 += kPrefetch) block(t0, std::integral_constant<int, kSide>{});
+        if (consumer)
+            for (; t0 + kPrefetch + TOFF <= t_side; t0 += kPrefetch)
+                block(t0, std::integral_constant<int, kSide>{});
     }
     // a producer whose stream had no steady block (a short last block) signals here
     if constexpr (HAND)

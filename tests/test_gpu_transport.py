@@ -78,6 +78,9 @@ def worker(rank, world, port, h, w, chunks, rule, seed, cfg, q):
 
 
 def run_ranks(world, h, w, chunks, rule, seed, **cfg):
+    # ranks sharing one GPU: classic row blocks (one waiting launch per device at a
+    # time, engine.cpp gol_create_group)
+    cfg.setdefault("handoff", 1)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
@@ -132,7 +135,7 @@ def digest_worker(rank, world, port, h, w, gens, seed, q):
         import __graft_entry__ as entry
         pkg = entry.load_package()
         with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, rank=rank, nranks=world,
-                        transport=gloo_exchange(rank, world)) as e:
+                        transport=gloo_exchange(rank, world), handoff=1) as e:
             e.init_random(seed)
             e.step(gens)
             d = e.digest()
