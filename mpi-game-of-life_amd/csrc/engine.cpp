@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -230,6 +231,7 @@ struct gol_engine {
         int32_t strips = 0, bands = 0, band_rows = 0, K = 0;
         uint32_t* flags = nullptr;
         uint32_t flag_base = 0;
+        hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering with the shared stream
     } res;
 
     std::vector<Region> user_regions;  // load/store mapping (own output rows)
@@ -813,15 +815,39 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
     const size_t tiles = (size_t)e->res.bands * (size_t)e->res.strips;
     HIP_TRY(hipMalloc(&e->res.flags, tiles * sizeof(uint32_t)));
     HIP_TRY(hipMemset(e->res.flags, 0, tiles * sizeof(uint32_t)));
+    HIP_TRY(hipEventCreateWithFlags(&e->res.ev_in, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&e->res.ev_out, hipEventDisableTiming));
     e->res.on = true;
     e->K = (uint32_t)e->res.K;
     return GOL_OK;
+}
+
+// The resident launches of every engine of this process on one device run on one
+// shared stream, in order: each needs all its tiles resident at once, one per CU,
+// so two side by side could each hold CUs the other's tiles wait for.  (Engines
+// of different processes on one GPU are not ordered: their resident waits are
+// bounded and a timeout is reported by gol_sync.)
+hipStream_t resident_stream(int device)
+{
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = streams.find(device);
+    if (it != streams.end()) return it->second;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    streams[device] = s;
+    return s;
 }
 
 // gol_step on a resident engine: one launch (per 2^30 generations).
 gol_status step_resident(gol_engine* e, uint64_t generations)
 {
     auto& r = e->res;
+    hipStream_t rs = resident_stream(e->device);
+    if (!rs) return fail(GOL_EHIP, "resident launch stream");
+    HIP_TRY(hipEventRecord(r.ev_in, e->stream));
+    HIP_TRY(hipStreamWaitEvent(rs, r.ev_in, 0));
     uint64_t left = generations;
     while (left > 0) {
         const int32_t g = (int32_t)std::min<uint64_t>(left, 1u << 30);
@@ -844,16 +870,18 @@ gol_status step_resident(gol_engine* e, uint64_t generations)
         a.birth = e->birth;
         a.survive = e->survive;
         hipEvent_t e0, e1;
-        GOL_TRY(timing_begin(e, e->stream, &e0, &e1));
-        HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, e->stream));
+        GOL_TRY(timing_begin(e, rs, &e0, &e1));
+        HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, rs));
         // lanes process every held row of every tile, every generation
         const double comp = (double)g * r.bands * r.strips * gol::kResWaves * r.rows * 64.0 * 64.0;
-        GOL_TRY(timing_end(e, e->stream, e0, e1, (double)e->H * (double)e->W * g, comp));
+        GOL_TRY(timing_end(e, rs, e0, e1, (double)e->H * (double)e->W * g, comp));
         const uint32_t epochs = (uint32_t)((g + r.K - 1) / r.K);
         r.flag_base += epochs;
         if (epochs & 1) e->cur ^= 1;
         left -= (uint64_t)g;
     }
+    HIP_TRY(hipEventRecord(r.ev_out, rs));
+    HIP_TRY(hipStreamWaitEvent(e->stream, r.ev_out, 0));
     return GOL_OK;
 }
 
@@ -1332,6 +1360,8 @@ void gol_destroy(gol_engine* e)
     }
     if (e->d_err) (void)hipFree(e->d_err);
     if (e->res.flags) (void)hipFree(e->res.flags);
+    for (hipEvent_t ev : {e->res.ev_in, e->res.ev_out})
+        if (ev) (void)hipEventDestroy(ev);
     for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.exec);
     if (e->d_acc) (void)hipFree(e->d_acc);
     if (e->d_flag) (void)hipFree(e->d_flag);

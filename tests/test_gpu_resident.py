@@ -11,9 +11,6 @@ fits, rules without and with births (B0 included: the dead border and columns
 beyond w must stay masked), flag counts carried across launches, odd/even
 epoch counts (buffer parity), and the hand-off under uneven load.
 """
-import threading
-
-import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -127,7 +124,8 @@ def test_resident_under_uneven_load(pkg, oracle):
     R = oracle.CONWAY
     g = oracle.bp_random(h, w, 9)
     want = oracle.bp_run(g, w, 300, R)
-    with pkg.Engine(16384, 16384, device=0, resident=1, streams=1) as big, \
+    # the busy engine uses classic row blocks: one waiting launch per device
+    with pkg.Engine(16384, 16384, device=0, resident=1, streams=1, handoff=1) as big, \
             pkg.Engine(h, w, rule=R, device=0) as e:
         assert e.resident is not None
         big.init_random(2)
@@ -138,3 +136,24 @@ def test_resident_under_uneven_load(pkg, oracle):
             got = e.store_packed()
             assert (got == want).all(), f"repetition {rep}"
         big.sync()
+
+
+def test_two_resident_engines_interleaved(pkg, oracle):
+    """Two resident engines of one process stepped without syncs in between: their
+    launches share one ordered stream per device (each needs every CU for its
+    tiles), so neither waits on tiles the other keeps off the chip."""
+    shapes = [(4096, 4096), (3000, 2500)]
+    fields = [oracle.bp_random(h, w, h + 1) for h, w in shapes]
+    engines = [pkg.Engine(h, w, rule=oracle.CONWAY, device=0) for h, w in shapes]
+    try:
+        for e, g in zip(engines, fields):
+            assert e.resident is not None
+            e.load_packed(g)
+        for chunk in (40, 7, 33):
+            for e in engines:
+                e.step(chunk)
+        for e, g, (h, w) in zip(engines, fields, shapes):
+            assert (e.store_packed() == oracle.bp_run(g, w, 80, oracle.CONWAY, threads=16)).all()
+    finally:
+        for e in engines:
+            e.close()
