@@ -1233,6 +1233,12 @@ gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int ra
     if (nranks > 1) {
         ncclUniqueId u;
         std::memcpy(&u, id, 128);
+        // the communicator binds to the calling thread's current device
+        hipError_t he = hipSetDevice(e->device);
+        if (he != hipSuccess) {
+            gol_destroy(e);
+            return fail(GOL_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(he));
+        }
         ncclResult_t r = ncclCommInitRank(&e->comm, nranks, u, rank);
         if (r != ncclSuccess) {
             gol_destroy(e);
