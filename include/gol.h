@@ -176,6 +176,15 @@ gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_pe
  * the planner resolved it): 1 = yes, 0 = every block recomputes its halo. */
 gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff);
 
+/* Age-skewed row blocks of full-depth launches (a one-round launch at 2
+ * wavefronts per SIMD: the units dispatched first win their SIMD's VALU
+ * arbitration and get longer blocks): *rows_old rows for the first *units_old
+ * units' blocks, *rows_young for the others; all 0 when the launches use equal
+ * blocks.  A composite engine reports its first stripe (which never skews: its
+ * stripes share the device).  Out pointers may be NULL. */
+gol_status gol_plan_skew(gol_engine* e, uint32_t* rows_old, uint32_t* rows_young,
+                         uint32_t* units_old);
+
 /* Resident plan (gol_config.resident): *on = 1 if gol_step runs the resident
  * kernel; then *bands x *strips tiles, one workgroup each (bands, strips may be
  * NULL).  A composite engine reports 0. */

@@ -34,7 +34,7 @@ EXPORTS = [
     "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
     "gol_create_rank", "gol_create_group", "gol_group_step", "gol_plan_info",
     "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
-    "gol_plan_resident",
+    "gol_plan_resident", "gol_plan_skew",
 ]
 
 
@@ -149,6 +149,7 @@ def lib():
     L.gol_plan_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.gol_plan_handoff.argtypes = [vp, ctypes.POINTER(u32)]
     L.gol_plan_resident.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    L.gol_plan_skew.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.gol_create_rank_transport.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32,
                                             ctypes.POINTER(Transport), ctypes.POINTER(vp)]
     L.gol_round_schedule.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32, u64, i32,
@@ -159,7 +160,7 @@ def lib():
                  "gol_sync", "gol_digest", "gol_set_timing", "gol_get_timing",
                  "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
                  "gol_create_group", "gol_group_step", "gol_plan_info", "gol_plan_handoff",
-                 "gol_plan_resident",
+                 "gol_plan_resident", "gol_plan_skew",
                  "gol_create_rank_transport", "gol_round_schedule"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -271,6 +272,10 @@ class Engine:
         _check(lib().gol_plan_resident(self._h, ctypes.byref(on), ctypes.byref(nb), ctypes.byref(ns)))
         # resident kernel: (bands, strips) of its tiles, or None
         self.resident = (nb.value, ns.value) if on.value else None
+        ro, ry, uo = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().gol_plan_skew(self._h, ctypes.byref(ro), ctypes.byref(ry), ctypes.byref(uo)))
+        # age-skewed row blocks: (rows_old, rows_young, units_old), or None
+        self.age_skew = (ro.value, ry.value, uo.value) if ro.value else None
 
     def close(self):
         if self._h:

@@ -28,6 +28,13 @@ namespace {
 
 thread_local std::string g_last_error;
 
+#if GOL_EXP
+// Dev timing builds (tools/exp_build.sh): device buffer the stencil kernel logs
+// per-wavefront (start, end, hardware id, unit) into; set by gol_dev_set_wave_log.
+uint64_t* g_dev_wave_log = nullptr;
+uint32_t* g_dev_prog = nullptr;  // GOL_EXP & 1024: per-SIMD progress words
+#endif
+
 // gol_create splits GLOBAL fields of at least this many rows into 2 same-device
 // stripes on 2 streams (measured +11% at 65536^2; no gain at <= 16384 rows,
 // profiles/r01/group_bench_*.jsonl)
@@ -179,6 +186,9 @@ struct gol_engine {
     gol_engine* up = nullptr;
     gol_engine* down = nullptr;
     bool grouped = false;
+    // other engines launch on this device concurrently (composite parts, group
+    // members sharing a GPU): the age skew's dispatch-order premise does not hold
+    bool shared_device = false;
     hipEvent_t ev_ready = nullptr, ev_copied = nullptr;
 
     // exchange/compute overlap (multi-rank): the last launch of a full round is
@@ -213,6 +223,10 @@ struct gol_engine {
         int64_t total_units = 0;
         bool multi_blk = false;  // some segment has more than one row block
         bool hand = false;       // the planner chose hand-off row blocks
+        // age-skewed row blocks (age_skew; 0 = off): the same blocks per strip, the
+        // first-dispatched units rows_old rows, the others rows_young (both = rpw
+        // mod the prefetch block, so the hand-off tail offset is rpw's)
+        int32_t rows_old = 0, rows_young = 0, units_old = 0;
         SegDesc* dev = nullptr;
     };
     std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: see RankGeom
@@ -371,6 +385,83 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
     return best[1][fh] <= best[0][fc] ? best_p[1][fh] : best_p[0][fc];
 }
 
+// Age-skewed row blocks.  A launch of one round at 2 wavefronts per SIMD first
+// gives every CU one workgroup, then a second: on each SIMD the wave of the first
+// workgroup (unit < 4 x CUs) is the older one and wins the VALU arbitration by age
+// (MI355X_MICROARCH.md, two waves per SIMD, item 2), so with equal blocks it ends
+// at ~0.82 of the launch and its partner finishes alone at half the SIMD's issue
+// rate (tools/wave_log.py: 69.8 vs 84.3 us at 8448 x 65536, 241 vs 295 us at
+// 33024; profiles/r02/wave_log_*.jsonl).  Balancing the pair by priority instead
+// (s_setprio flips, closed loop) was measured 9-10% slower.  So the older units
+// get longer blocks: the bottom blocks of each strip whose units are < units_old
+// have rows_old rows, the others R, with the young/old rate ratio kAgeRate fitted
+// to the pairs' end stamps; the block count, and so the units, stay as planned.
+// Returns rows_old (0 = no skew).  GOL_DEV_AGE_SKEW overrides kAgeRate (dev A/B;
+// 0 turns the skew off).
+constexpr double kAgeRate = 0.78;
+
+constexpr double kHandSkewCost = 1.05;
+
+struct Skew {
+    int64_t rows_old = 0, rows_young = 0, nblk = 0;  // rows_old 0 = no skew
+    double t = 0;  // modelled launch time, in rows of the kernel kind's cost
+};
+
+Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, int occ, int K,
+              int planes, bool hand)
+{
+    Skew best_s;
+    // young/old issue-rate ratio of a SIMD's pair (end-stamp fit; the in-process
+    // A/B optimum, profiles/r02/ab_skew.jsonl)
+    double rho = hand ? 0.78 : 0.72;
+    if (const char* v = std::getenv("GOL_DEV_AGE_SKEW")) rho = std::atof(v);
+    const int64_t rows = sg.out_hi - sg.out_lo;
+    if (rho <= 0 || rho >= 1 || occ != 2 || rows <= 0) return best_s;
+    const int pf = gol::prefetch_of(K, planes);
+    auto cost = [&](int64_t r) { return hand ? 1.02 * (double)r + 10.0 : (double)(r + K + 4); };
+    auto fits = [&](int64_t r) { return r >= std::max(8, K + 2) && (!hand || handoff_fits(r, K, planes)); };
+    double best = cost(R) / rho;  // equal blocks: the young wave's time
+    // block counts up to the planned one, as long as the launch stays one round of
+    // more than units_old wavefronts
+    const int64_t nb0 = (rows + R - 1) / R;
+    for (int64_t nblk = std::max<int64_t>(2, nb0 - nb0 / 4); nblk <= nb0; ++nblk) {
+        const int64_t units = nblk * strips;
+        if (units <= units_old || units > 2 * units_old) continue;
+        auto jold = [&](int64_t s) {
+            return std::min<int64_t>(nblk, std::max<int64_t>(0, (units_old - s + strips - 1) / strips));
+        };
+        for (int64_t ro = R; ro <= 2 * R; ro += pf) {
+            // the young length: the least in ro's class mod pf (= R's, so the launch
+            // keeps R's hand-off tail offset) that covers every strip
+            int64_t ry = 1;
+            bool ok = true;
+            for (int64_t s = 0; s < strips && ok; ++s) {
+                const int64_t jo = jold(s), ny = nblk - jo;
+                if (ny == 0)
+                    ok = jo * ro >= rows;
+                else
+                    ry = std::max<int64_t>(ry, (rows - jo * ro + ny - 1) / ny);
+            }
+            if (!ok) continue;
+            ry += ((ro - ry) % pf + pf) % pf;
+            if (ry >= ro || !fits(ry) || !fits(ro)) continue;
+            // every strip's blocks cover the rows and its last block is not empty
+            for (int64_t s = 0; s < strips && ok; ++s) {
+                const int64_t jo = jold(s), ny = nblk - jo;
+                const int64_t total = ny * ry + jo * ro, last = jo ? ro : ry;
+                ok = total >= rows && total - last < rows;
+            }
+            if (!ok) continue;
+            const double t = std::max(cost(ro), cost(ry) / rho);
+            if (t < best * 0.995) {
+                best = t;
+                best_s = {ro, ry, nblk, t};
+            }
+        }
+    }
+    return best_s;
+}
+
 gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
 {
     int cus = 0;
@@ -392,6 +483,27 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                           .hand
                       ? 2
                       : 1;
+    // With age-skewed blocks both kinds gain, classic blocks more (their halo
+    // recompute is per block, and the old units' longer blocks amortize it): per
+    // modelled row a skewed hand-off launch ran ~5% slower than a skewed classic one
+    // at the per-GPU shapes 8448..33024 x 65536 (profiles/r02/ab_skew.jsonl), which
+    // puts the crossover between 16640 rows (hand-off) and 33024 (classic).  When
+    // both kinds skew, the modelled times decide.
+    if (e->handoff == 0 && handoff == 2 && raw.size() >= 1 && raw[0].size() == 1 &&
+        !e->rows_per_wave && !e->shared_device) {
+        const int64_t first = (int64_t)gol::kWavesPerBlock * cus;
+        Skew sk[2];
+        for (int hand = 0; hand <= 1; ++hand) {
+            const RowPlan rp = pick_rows_per_wave(raw[0], e->ng, (int)e->K, e->planes, occ_c, occ_h,
+                                                  4 * cus, 0, e->lane_shift, hand ? 2u : 1u);
+            if (rp.hand != (hand != 0)) break;
+            std::vector<SegDesc> segs = raw[0];
+            finish_segs(segs, rp.rpw, rp.groups);
+            sk[hand] = age_skew(segs[0], rp.rpw, rp.groups, first, hand ? occ_h : occ_c, (int)e->K,
+                                e->planes, hand != 0);
+        }
+        if (sk[0].rows_old && sk[1].rows_old && sk[0].t < sk[1].t * kHandSkewCost) handoff = 1;
+    }
     for (size_t pi = 0; pi < raw.size(); ++pi) {
         const auto& r = raw[pi];
         gol_engine::Plan p;
@@ -408,6 +520,19 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         p.hand = rp.hand;
         finish_segs(p.segs, p.rpw, p.groups);
         p.total_units = plan_units(p.segs, p.groups);
+        if (!band && p.segs.size() == 1 && !e->rows_per_wave && !e->shared_device) {
+            const int occ = p.hand ? occ_h : occ_c;
+            const int64_t first = (int64_t)gol::kWavesPerBlock * cus;  // one workgroup per CU
+            const Skew sk = age_skew(p.segs[0], p.rpw, p.groups, first, occ, (int)e->K,
+                                     e->planes, p.hand);
+            if (sk.rows_old) {
+                p.rows_young = (int32_t)sk.rows_young;
+                p.rows_old = (int32_t)sk.rows_old;
+                p.units_old = (int32_t)first;
+                p.segs[0].nblk = sk.nblk;
+                p.total_units = plan_units(p.segs, p.groups);
+            }
+        }
         for (const auto& sg : p.segs) {
             p.multi_blk |= sg.nblk > 1;
             // own rows of a segment: rank engines [Hx, Hx+R); REF_STRIPES the
@@ -434,6 +559,12 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         e->plans.push_back(p);
     }
     HIP_TRY(hipMalloc(&e->d_err, sizeof(int)));
+#if GOL_EXP
+    if (!g_dev_prog) {
+        HIP_TRY(hipMalloc(&g_dev_prog, 8192 * 2 * sizeof(uint32_t)));
+        HIP_TRY(hipMemset(g_dev_prog, 0, 8192 * 2 * sizeof(uint32_t)));
+    }
+#endif
     HIP_TRY(hipMemset(e->d_err, 0, sizeof(int)));
     if (any_hand && max_units > 0) {
         const size_t slot = (size_t)2 * (e->K - 1) * 64 * (size_t)(e->planes / 2);
@@ -916,6 +1047,15 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         a.side_slot = (int64_t)2 * (depth - 1) * 64 * (e->planes / 2);
         a.tail_off = gol::handoff_toff(p.rpw, (int)depth, e->planes);
     }
+    if (p.rows_old) {
+        a.rows_per_wave = p.rows_young;
+        a.rows_old = p.rows_old;
+        a.units_old = p.units_old;
+    }
+#if GOL_EXP
+    a.wlog = g_dev_wave_log;
+    a.prog = g_dev_prog;
+#endif
     hipEvent_t e0, e1;
     GOL_TRY(timing_begin(e, s, &e0, &e1));
     HIP_TRY(gol::launch_life(a, (int)depth, e->rule, e->planes, hand, s));
@@ -1190,7 +1330,7 @@ namespace {
 
 // Geometry + device state of stripe `rank` of `nranks` (no transport yet).
 gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
-                            gol_engine** out)
+                            gol_engine** out, bool shared_device = false)
 {
     *out = nullptr;
     gol_status st = check_cfg(cfg);
@@ -1208,6 +1348,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     e->row0 = g.row0;
     e->R = g.R;
     e->Hx = g.Hx;
+    e->shared_device = shared_device;
     st = init_common(e, h, w, cfg, &g);
     if (st != GOL_OK) {
         std::string msg = g_last_error;
@@ -1284,14 +1425,17 @@ gol_status gol_create_group(uint64_t h, uint64_t w, const gol_config* cfg, int n
     // hold each other's slots).  Members sharing a device run concurrently, so
     // only the first member on each device keeps hand-off blocks.
     std::vector<int> devs;
+    for (int r = 0; r < nranks; ++r) {
+        int d = devices ? devices[r] : (cfg->device >= 0 ? cfg->device : -1);
+        if (d < 0 && hipGetDevice(&d) != hipSuccess) d = -1;
+        devs.push_back(d);
+    }
     for (int r = 0; r < nranks && st == GOL_OK; ++r) {
         gol_config c = *cfg;
         c.device = devices ? devices[r] : (cfg->device >= 0 ? cfg->device : -1);
-        int d = c.device;
-        if (d < 0 && hipGetDevice(&d) != hipSuccess) d = -1;
-        if (std::find(devs.begin(), devs.end(), d) != devs.end()) c.handoff = 1;
-        devs.push_back(d);
-        st = make_rank_engine(h, w, &c, r, nranks, &engines[r]);
+        if (std::find(devs.begin(), devs.begin() + r, devs[r]) != devs.begin() + r) c.handoff = 1;
+        st = make_rank_engine(h, w, &c, r, nranks, &engines[r],
+                              std::count(devs.begin(), devs.end(), devs[r]) > 1);
     }
     for (int r = 0; r < nranks && st == GOL_OK; ++r) {
         gol_engine* e = engines[r];
@@ -1986,6 +2130,19 @@ gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_pe
     return GOL_OK;
 }
 
+gol_status gol_plan_skew(gol_engine* e, uint32_t* rows_old, uint32_t* rows_young,
+                         uint32_t* units_old)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) return gol_plan_skew(e->parts[0], rows_old, rows_young, units_old);
+    if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
+    const auto& p = e->nranks > 1 ? e->plans[e->Hx - 1] : e->plans[0];
+    const bool on = !e->res.on && p.rows_old;
+    if (rows_old) *rows_old = on ? (uint32_t)p.rows_old : 0u;
+    if (rows_young) *rows_young = on ? (uint32_t)p.rows_young : 0u;
+    if (units_old) *units_old = on ? (uint32_t)p.units_old : 0u;
+    return GOL_OK;
+}
 gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint32_t* strips)
 {
     if (!e || !on) return fail(GOL_EINVAL, "null argument");
@@ -2014,3 +2171,13 @@ gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff)
 }
 
 }  // extern "C"
+
+#if GOL_EXP
+// Dev timing builds only: log every stencil wavefront's (start, end) s_memrealtime
+// stamps, HW_ID | XCC_ID << 32 and unit into `dev` (4 words per wavefront; null
+// turns the log off).  Not part of include/gol.h.
+extern "C" __attribute__((visibility("default"))) void gol_dev_set_wave_log(void* dev)
+{
+    g_dev_wave_log = static_cast<uint64_t*>(dev);
+}
+#endif

@@ -61,6 +61,11 @@ struct StepArgs {
     uint64_t lastmask[2]; // stored-form valid bits of the last group's words
     int64_t rows_per_wave;
     int64_t total_units;  // wavefronts in the launch
+    // Age-skewed row blocks (one-segment launches of one round, engine.cpp
+    // age_skew): units below units_old start first on their SIMD, win its VALU
+    // arbitration and get rows_old rows; the others rows_per_wave.  0 = off.
+    int32_t rows_old;
+    int32_t units_old;
     uint32_t birth, survive;
     // Row-block hand-off (kernels instantiated with HAND = true; see
     // life_stencil.h): each wavefront's slot of side rows, its ready flag, and a
@@ -69,6 +74,8 @@ struct StepArgs {
     uint32_t* flags;      // total_units words, zeroed before every launch
     int* err;
     int64_t side_slot;    // words per slot: 2 (K-1) rows x 64 lanes x NP/2 words
+    uint64_t* wlog;       // dev timing builds only (GOL_EXP & 128): 4 words per wavefront
+    uint32_t* prog;       // dev (GOL_EXP & 1024): per-SIMD wave progress, 2 words per SIMD
 };
 
 // Fused depths with an instantiated kernel, largest first.  The shipped library

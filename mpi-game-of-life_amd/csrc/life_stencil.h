@@ -310,7 +310,10 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2;
 
 // Dev timing experiments only (tools/exp_build.sh; results are NOT valid): bit 0
 // skips the consumer's wait, bit 1 the producer's drain + flag, bit 2 the
-// side-row stores, bit 3 the consumer's tail.
+// side-row stores, bit 3 the consumer's tail; bit 7 logs every wavefront's start/end
+// stamps and hardware id (gol_dev_set_wave_log), bits 8/9 alternate s_setprio
+// between the two waves of a SIMD every steady block, bit 10 balances them closed-loop
+// (each takes priority while it is not ahead of its partner).
 #ifndef GOL_EXP
 #define GOL_EXP 0
 #endif
@@ -330,6 +333,32 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     const int64_t unit =
         (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (unit >= a.total_units) return;
+#if GOL_EXP & 128
+    const uint64_t wl_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+#if GOL_EXP & (256 | 512)
+    // priority alternation between the two waves of a SIMD: parity from the wave
+    // slot (HW_ID.WAVE_ID, 256) or from dispatch order (first half of the grid, 512)
+    const uint32_t prio_par = (GOL_EXP & 256)
+                                  ? (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4) & 1u)
+                                  : (blockIdx.x < gridDim.x / 2 ? 0u : 1u);
+#endif
+#if GOL_EXP & 1024
+    // closed-loop balance of the two waves of a SIMD: each publishes its count of
+    // steady blocks in its SIMD's slot (HW_ID wave slot & 1) and takes priority
+    // while it is not ahead of its partner
+    uint32_t* prog_me;
+    const uint32_t* prog_mate;
+    {
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 7;
+        const uint32_t simd = ((((xcc * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 +
+                                ((hw >> 8) & 15)) * 4 + ((hw >> 4) & 3));
+        prog_me = a.prog + simd * 2 + (hw & 1);
+        prog_mate = a.prog + simd * 2 + ((hw & 1) ^ 1);
+    }
+    uint32_t prog_n = 0, prog_m = 0;
+#endif
 
     int sidx = 0;
     for (int j = 1; j < a.nseg; ++j)
@@ -364,8 +393,20 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     const uint32_t voff = (uint32_t)(qc * G * 8);
     const uint32_t voff_side = (uint32_t)(lane * G * 8);
 
-    const int64_t rb = sg.out_lo + blk * a.rows_per_wave;
-    const int64_t re = min(rb + a.rows_per_wave, sg.out_hi);
+    // row block [rb, re): rows_per_wave rows each, or with age-skewed blocks
+    // (one segment) the bottom blocks of a strip whose units start first (u <
+    // units_old, the older wave of their SIMD) rows_old rows each
+    int64_t rb = sg.out_lo + blk * a.rows_per_wave, rlen = a.rows_per_wave;
+    if (a.rows_old) {
+        const int64_t s = u % a.strips;
+        const int64_t jo = min(sg.nblk, max((int64_t)0, (a.units_old - s + a.strips - 1) / a.strips));
+        const int64_t ny = sg.nblk - jo;  // young blocks, on top
+        if (blk >= ny) {
+            rb = sg.out_lo + ny * a.rows_per_wave + (blk - ny) * a.rows_old;
+            rlen = a.rows_old;
+        }
+    }
+    const int64_t re = min(rb + rlen, sg.out_hi);
     // step counts and indices are 32-bit (a block has at most rows_per_wave + 2K
     // steps): uniform 32-bit compares stay on the scalar unit, 64-bit ones do not
     const int32_t T = (int32_t)(re - rb) + 2 * K;  // steps (input rows of a classic block)
@@ -540,6 +581,29 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
                 }
             }
         }
+#if GOL_EXP & (256 | 512)
+        if constexpr (!kGuard) {
+            if (__builtin_amdgcn_readfirstlane(((uint32_t)t0 / kPrefetch ^ prio_par) & 1u))
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
+#endif
+#if GOL_EXP & 1024
+        if constexpr (!kGuard) {
+            // the partner's count loaded one block ago (its latency hidden by this
+            // block's compute); then publish ours and load theirs for the next block
+            if (__builtin_amdgcn_readfirstlane(prog_m) < prog_n)
+                __builtin_amdgcn_s_setprio(0);
+            else
+                __builtin_amdgcn_s_setprio(1);
+            ++prog_n;
+            if (lane == 0)
+                __hip_atomic_store(prog_me, prog_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            prog_m = __hip_atomic_load(const_cast<uint32_t*>(prog_mate), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+#endif
         if constexpr (!kGuard) {
             __builtin_amdgcn_sched_barrier(0);
             // hand-off signalling between this block's compute and its stores: the
@@ -630,6 +694,16 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
             for (int tau0 = 0; tau0 < kSideRows; tau0 += kPrefetch) tail(tau0);
         }
     }
+#if GOL_EXP & 128
+    if (a.wlog && lane == 0) {
+        uint64_t* wl = a.wlog + unit * 4;
+        wl[0] = wl_t0;
+        wl[1] = __builtin_amdgcn_s_memrealtime();
+        wl[2] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) |
+                ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) << 32);
+        wl[3] = (uint64_t)blk | ((uint64_t)blockIdx.x << 32);
+    }
+#endif
 }
 
 }  // namespace

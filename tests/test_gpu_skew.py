@@ -1,0 +1,70 @@
+"""GPU parity of age-skewed row blocks (engine.cpp age_skew, life_stencil.h).
+
+A one-round launch at 2 wavefronts per SIMD gives the units dispatched first
+(the older wave of each SIMD) longer row blocks than the others.  The blocks of a
+strip then have two lengths and the block count differs from ceil(rows / R), so
+the row ranges, the hand-off roles and the last (truncated) block all move.  The
+per-GPU stripe shapes of the 2/4/8-way 65536^2 split are checked bit-exact
+against the CPU oracle (one K = 16 launch), and over several launches against
+the same engine with equal blocks.
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+W = 65536
+THREADS = 16
+
+
+def rule_of(oracle, rule):
+    return oracle.REF_RULE if rule == "ref" else oracle.CONWAY
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+@pytest.mark.parametrize("handoff", [1, 2])
+@pytest.mark.parametrize("rows", [8448, 16640])
+def test_skewed_stripe_vs_oracle(pkg, oracle, rows, handoff, rule):
+    R = rule_of(oracle, rule)
+    with pkg.Engine(rows, W, rule=R, device=0, handoff=handoff, streams=1) as e:
+        assert e.tb_depth == 16 and e.age_skew is not None, (e.tb_depth, e.age_skew)
+        ro, ry, uo = e.age_skew
+        assert ro > ry > 0 and uo > 0
+        e.init_random(3)
+        e.step(16)  # one K = 16 launch
+        got = e.digest()
+    g = oracle.bp_run(oracle.bp_random(rows, W, 3), W, 16, R, threads=THREADS)
+    assert got == oracle.bp_digest(g, W)
+
+
+@pytest.mark.parametrize("rows", [8448, 12288, 33024])
+def test_skewed_equals_equal_blocks(pkg, monkeypatch, rows):
+    """Several full-depth launches and a remainder (Conway keeps the field
+    changing) with the planner's automatic choice, against equal blocks."""
+    gens = 5 * 16 + 8
+    with pkg.Engine(rows, W, rule=pkg.CONWAY, device=0, streams=1) as e:
+        assert e.age_skew is not None
+        e.init_random(5)
+        e.step(gens)
+        got = e.digest()
+    monkeypatch.setenv("GOL_DEV_AGE_SKEW", "0")
+    with pkg.Engine(rows, W, rule=pkg.CONWAY, device=0, streams=1) as e:
+        assert e.age_skew is None
+        e.init_random(5)
+        e.step(gens)
+        assert e.digest() == got
+
+
+def test_no_skew_when_launches_share_the_device(pkg):
+    """Composite stripes and group members on one GPU launch concurrently, so the
+    dispatch-order premise does not hold: equal blocks."""
+    with pkg.Engine(W, W, device=0) as e:
+        assert e.age_skew is None
+    with pkg.Group(16640 * 2, W, 2) as grp:
+        assert all(m.age_skew is None for m in grp.members)
+
+
+def test_no_skew_for_forced_rows_or_multi_round(pkg):
+    with pkg.Engine(8448, W, device=0, streams=1, rows_per_wave=74) as e:
+        assert e.age_skew is None  # a caller's rows_per_wave is kept as given
+    with pkg.Engine(2048, W, device=0, streams=1, resident=1) as e:
+        assert e.age_skew is None  # fewer units than one workgroup per CU x 4

@@ -10,6 +10,7 @@ for N in "$@"; do
   D=/tmp/golexp$N
   rm -rf $D && mkdir -p $D && cp -r $ROOT/mpi-game-of-life_amd $D/ && cp -r $ROOT/include $D/
   rm -rf $D/mpi-game-of-life_amd/build $D/mpi-game-of-life_amd/*.so
-  make -s -C $D/mpi-game-of-life_amd -j8 libgol.so KFLAGS="-mllvm -pragma-unroll-threshold=1000000 -DGOL_EXP=$N"
+  make -s -C $D/mpi-game-of-life_amd -j8 libgol.so KFLAGS="-mllvm -pragma-unroll-threshold=1000000 -DGOL_EXP=$N" \
+       CXXFLAGS="-O3 -std=c++17 -fPIC -DGOL_EXP=$N"
   cp $D/mpi-game-of-life_amd/libgol.so $ROOT/mpi-game-of-life_amd/libgol_exp$N.so
 done

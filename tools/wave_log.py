@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Dev tool: per-wavefront timing of one stencil launch (exp builds with
+GOL_EXP & 128, tools/exp_build.sh), and the wall-clock rate of the same shape.
+
+Each wavefront logs its s_memrealtime start/end stamps (100 MHz), HW_ID and
+XCC_ID.  Wavefronts sharing a SIMD (same XCC, SE, SH, CU, SIMD) are paired, and
+the tool reports how long the first-finishing wave of a pair ends before the
+second (the time its partner runs alone on the SIMD), the spread of start and
+end stamps, and the launch span.
+
+    GOL_LIB=mpi-game-of-life_amd/libgol_exp128.so python tools/wave_log.py --rows 8448
+"""
+import argparse
+import collections
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import __graft_entry__ as entry  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rows", type=int, default=8448)
+    p.add_argument("--width", type=int, default=65536)
+    p.add_argument("--handoff", type=int, default=0)
+    p.add_argument("--streams", type=int, default=1)
+    p.add_argument("--gens", type=int, default=512)
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--tag", default="")
+    p.add_argument("--cus", type=int, default=256)
+    a = p.parse_args()
+    import torch
+    pkg = entry.load_package()
+    L = pkg.lib()
+    e = pkg.Engine(a.rows, a.width, device=0, handoff=a.handoff, streams=a.streams)
+    e.init_random(1)
+    e.step(a.gens)
+    e.sync()
+    ts = []
+    for _ in range(a.rounds):
+        t0 = time.perf_counter()
+        e.step(a.gens)
+        e.sync()
+        ts.append(time.perf_counter() - t0)
+    tcups = a.rows * a.width * a.gens / statistics.median(ts) / 1e12
+    log = torch.zeros(4 * 65536, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    L.gol_dev_set_wave_log(ctypes.c_void_p(log.data_ptr()))
+    e.step(e.tb_depth)  # one full-depth launch
+    e.sync()
+    L.gol_dev_set_wave_log(ctypes.c_void_p(0))
+    w = log.view(-1, 4).cpu().numpy().astype("uint64")
+    w = w[w[:, 0] != 0]
+    start, end = w[:, 0].astype("int64"), w[:, 1].astype("int64")
+    hw = [int(x) for x in w[:, 2]]
+    t0 = start.min()
+    dur_us = (end - start) / 100.0  # s_memrealtime: 100 MHz
+    # xcc | se, sh, cu, simd (HW_ID bits 15:4 without the pipe id)
+    simd_key = [((x >> 32) << 16) | (((x & 0xFFFF) >> 4) & ~0xC) for x in hw]
+    pairs = collections.defaultdict(list)
+    for i, k in enumerate(simd_key):
+        pairs[int(k)].append(i)
+    solo, lead_share = [], []
+    occ = collections.Counter(len(v) for v in pairs.values())
+    for v in pairs.values():
+        if len(v) != 2:
+            continue
+        i, j = v
+        first, second = sorted((end[i], end[j]))
+        span = max(end[i], end[j]) - min(start[i], start[j])
+        solo.append((second - first) / 100.0)
+        lead_share.append((second - first) / span)
+    rec = {
+        "tag": a.tag, "lib": os.path.basename(os.environ.get("GOL_LIB", "libgol.so")),
+        "shape": f"{a.rows}x{a.width}", "tb_depth": e.tb_depth, "rows_per_wave": e.rows_per_wave,
+        "handoff": e.handoff, "tcups_wall_median": round(tcups, 2),
+        "waves": int(len(w)), "simds_by_waves": {str(k): n for k, n in sorted(occ.items())},
+        "launch_span_us": round((end.max() - t0) / 100.0, 2),
+        "start_spread_us": round((start.max() - t0) / 100.0, 2),
+        "wave_us": {"min": round(float(dur_us.min()), 2), "median": round(float(statistics.median(dur_us)), 2),
+                    "max": round(float(dur_us.max()), 2)},
+        "end_us_quantiles": [round(float(x), 2) for x in
+                             ((sorted(end - t0)[int(q * (len(end) - 1))]) / 100.0
+                              for q in (0.0, 0.1, 0.25, 0.5, 0.75, 0.9, 1.0))],
+        "pair_solo_us": ({"median": round(statistics.median(solo), 2), "max": round(max(solo), 2),
+                          "mean": round(statistics.mean(solo), 2)} if solo else None),
+        "pair_solo_share_median": round(statistics.median(lead_share), 3) if lead_share else None,
+        "wave_slot_ids": dict(collections.Counter(int(x) & 15 for x in hw)),
+    }
+    # dispatch order vs wave slot: which workgroups got slot 0 (the older wave of a
+    # pair), and the median end stamp of each slot
+    wg = w[:, 3].astype("int64") >> 32
+    slot = [x & 15 for x in hw]
+    ncu = int(a.cus)
+    rec["slot0_wg_lt_ncu"] = round(sum(1 for i, s in enumerate(slot) if s == 0 and wg[i] < ncu)
+                                   / max(1, sum(1 for s in slot if s == 0)), 4)
+    rec["slot1_wg_ge_ncu"] = round(sum(1 for i, s in enumerate(slot) if s == 1 and wg[i] >= ncu)
+                                   / max(1, sum(1 for s in slot if s == 1)), 4)
+    for sl in (0, 1):
+        ends = [float(end[i] - t0) / 100.0 for i, s in enumerate(slot) if s == sl]
+        if ends:
+            rec[f"slot{sl}_end_us_median"] = round(statistics.median(ends), 2)
+    print(json.dumps(rec), flush=True)
+    e.close()
+
+
+if __name__ == "__main__":
+    main()
