@@ -420,17 +420,23 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
     const int pf = gol::prefetch_of(K, planes);
     auto cost = [&](int64_t r) { return hand ? 1.02 * (double)r + 10.0 : (double)(r + K + 4); };
     auto fits = [&](int64_t r) { return r >= std::max(8, K + 2) && (!hand || handoff_fits(r, K, planes)); };
-    double best = cost(R) / rho;  // equal blocks: the young wave's time
-    // block counts up to the planned one, as long as the launch stays one round of
-    // more than units_old wavefronts
+    // the planned equal blocks: nw wavefronts per SIMD run as pairs (old rate 1,
+    // young rho) with refills, and the last pair's young wave ends alone
     const int64_t nb0 = (rows + R - 1) / R;
-    for (int64_t nblk = std::max<int64_t>(2, nb0 - nb0 / 4); nblk <= nb0; ++nblk) {
+    const double nw = std::ceil((double)(nb0 * strips) / (double)units_old);
+    double best = std::max(0.0, nw - 2) * cost(R) / (1 + rho) + cost(R) / rho;
+    // every block count of one round of more than units_old (= one per SIMD)
+    // wavefronts: the old blocks from the mean length to twice it
+    for (int64_t nblk = std::max<int64_t>(2, units_old / strips + 1); nblk * strips <= 2 * units_old;
+         ++nblk) {
         const int64_t units = nblk * strips;
-        if (units <= units_old || units > 2 * units_old) continue;
+        if (units <= units_old) continue;
+        const int64_t mean = (rows + nblk - 1) / nblk;
+        const int64_t ro0 = mean + ((R - mean) % pf + pf) % pf;
         auto jold = [&](int64_t s) {
             return std::min<int64_t>(nblk, std::max<int64_t>(0, (units_old - s + strips - 1) / strips));
         };
-        for (int64_t ro = R; ro <= 2 * R; ro += pf) {
+        for (int64_t ro = ro0; ro <= 2 * mean + pf; ro += pf) {
             // the young length: the least in ro's class mod pf (= R's, so the launch
             // keeps R's hand-off tail offset) that covers every strip
             int64_t ry = 1;
@@ -460,6 +466,50 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
         }
     }
     return best_s;
+}
+
+// Whether a single-stream GLOBAL engine of this field would run age-skewed
+// one-round launches (build_plans' choice, without allocating it).  gol_create
+// then prefers it to the composite engine: 65536^2 ran 133.6 TCUPS on one stream
+// with skewed blocks against 130.6 as 2 same-device stripes (profiles/r02/
+// ab_skew_single_vs_composite.jsonl) -- the skew hides the pair tails that the
+// second stream's launches otherwise fill.
+bool single_stream_skews(uint64_t h, uint64_t w, const gol_config* cfg)
+{
+    if (cfg->rows_per_wave || h > (uint64_t)INT32_MAX) return false;
+    const Layout lay = auto_layout(h, cfg);
+    const int K = (int)lay.K, planes = lay.planes;
+    if (!gol::life_has_kernel(K, planes)) return false;
+    gol::RuleKind rule = gol::RULE_GENERIC;
+    if (cfg->birth_mask == GOL_REF_BIRTH && cfg->survive_mask == GOL_REF_SURVIVE)
+        rule = gol::RULE_REF;
+    else if (cfg->birth_mask == GOL_CONWAY_BIRTH && cfg->survive_mask == GOL_CONWAY_SURVIVE)
+        rule = gol::RULE_CONWAY;
+    int dev = cfg->device, cus = 0;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    const uint64_t wq = (w + 63) / 64, G = (uint64_t)planes / 2, ng = (wq + G - 1) / G;
+    const int shift = cfg->strip_lanes == 64 ? 0 : cfg->strip_lanes == 32 ? 1
+                    : cfg->strip_lanes == 16 ? 2 : -1;
+    const bool hand_ok = gol::handoff_kernel_exists(K, rule);
+    const int occ_c = gol::life_blocks_per_cu(K, rule, planes, false);
+    const int occ_h = hand_ok ? gol::life_blocks_per_cu(K, rule, planes, true) : 0;
+    SegDesc s{};
+    s.in_rows = s.field_h = s.out_hi = (int64_t)h;
+    for (int hand = 0; hand <= 1; ++hand) {
+        if ((hand && (cfg->handoff == 1 || !hand_ok)) || (!hand && cfg->handoff == 2)) continue;
+        const RowPlan rp = pick_rows_per_wave({s}, ng, K, planes, occ_c, occ_h, 4 * cus, 0, shift,
+                                              hand ? 2u : 1u);
+        if (rp.hand != (hand != 0)) continue;
+        std::vector<SegDesc> segs{s};
+        finish_segs(segs, rp.rpw, rp.groups);
+        if (age_skew(segs[0], rp.rpw, rp.groups, (int64_t)gol::kWavesPerBlock * cus,
+                     hand ? occ_h : occ_c, K, planes, hand != 0)
+                .rows_old)
+            return true;
+    }
+    return false;
 }
 
 gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
@@ -502,7 +552,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
             sk[hand] = age_skew(segs[0], rp.rpw, rp.groups, first, hand ? occ_h : occ_c, (int)e->K,
                                 e->planes, hand != 0);
         }
-        if (sk[0].rows_old && sk[1].rows_old && sk[0].t < sk[1].t * kHandSkewCost) handoff = 1;
+        if (sk[0].rows_old && (!sk[1].rows_old || sk[0].t < sk[1].t * kHandSkewCost)) handoff = 1;
     }
     for (size_t pi = 0; pi < raw.size(); ++pi) {
         const auto& r = raw[pi];
@@ -1201,7 +1251,10 @@ gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine*
     if (!e) return fail(GOL_ENOMEM, "host allocation");
     e->R = h;
     uint32_t S = cfg->streams;
-    if (S == 0) S = (cfg->semantics == GOL_SEM_GLOBAL && h >= kCompositeMinRows) ? 2 : 1;
+    if (S == 0)
+        S = (cfg->semantics == GOL_SEM_GLOBAL && h >= kCompositeMinRows && !single_stream_skews(h, w, cfg))
+                ? 2
+                : 1;
     if (S > 1 && cfg->semantics == GOL_SEM_GLOBAL && h / S >= 256) {
         // composite: S same-device stripes with deep halos, advanced together
         gol_config c = *cfg;

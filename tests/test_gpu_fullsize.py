@@ -1,8 +1,9 @@
 """GPU parity at the benchmark sizes (BASELINE.json configs[2..4]).
 
-The timed path itself: gol_create(65536, 65536) with defaults is the composite
-engine (2 same-device stripes on 2 streams, 256-row halo rounds, K = 16, row
-blocks as the planner picks them) -- exactly what bench.py measures.  Checked
+The timed path itself: gol_create(65536, 65536) with defaults is one stream of
+K = 16 launches with age-skewed row blocks (engine.cpp age_skew) -- exactly what
+bench.py measures; the 2-stripe composite engine (streams=2: 2 same-device
+stripes on 2 streams, 256-row halo rounds) is checked the same way.  Checked
   * against the CPU oracle after one step(16) call (the K = 16 kernel runs);
   * after 600 more generations (two overlapped 256-generation rounds and a
     partial one) against a streams=1, tb_depth=1, classic-block engine, which the
@@ -28,15 +29,17 @@ def digest_of(pkg, h, w, rule, gens, seed=1, **kw):
         return e.digest()
 
 
+@pytest.mark.parametrize("streams", [0, 2])
 @pytest.mark.parametrize("rule", ["ref", "conway"])
-def test_c3_default_engine_vs_oracle_and_depth1(pkg, oracle, rule):
+def test_c3_default_engine_vs_oracle_and_depth1(pkg, oracle, rule, streams):
     R = oracle.REF_RULE if rule == "ref" else oracle.CONWAY
-    with pkg.Engine(N, N, rule=R, device=0) as e:
+    with pkg.Engine(N, N, rule=R, device=0, streams=streams) as e:
         assert e.tb_depth == 16 and e.resident is None, (e.tb_depth, e.resident)
+        assert (e.age_skew is not None) == (streams == 0), e.age_skew
         e.init_random(1)
         e.step(16)  # one full-depth launch per stripe
         d16 = e.digest()
-        e.step(600)  # 2 overlapped 256-generation rounds + a partial one
+        e.step(600)  # composite: 2 overlapped 256-generation rounds + a partial one
         d616 = e.digest()
     g = oracle.bp_run(oracle.bp_random(N, N, 1), N, 16, R, threads=THREADS)
     assert d16 == oracle.bp_digest(g, N)

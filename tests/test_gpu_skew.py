@@ -54,10 +54,22 @@ def test_skewed_equals_equal_blocks(pkg, monkeypatch, rows):
         assert e.digest() == got
 
 
+def test_default_c3_engine_is_one_skewed_stream(pkg):
+    """gol_create(65536, 65536) runs one stream of skewed one-round launches
+    (it beats the 2-stripe composite), and says so in its plan."""
+    with pkg.Engine(W, W, device=0) as e:
+        assert e.age_skew is not None and e.tb_depth == 16
+        e.set_timing(1)
+        e.init_random(1)
+        e.step(16)
+        e.sync()
+        assert e.timing()["streams"] == 1
+
+
 def test_no_skew_when_launches_share_the_device(pkg):
     """Composite stripes and group members on one GPU launch concurrently, so the
     dispatch-order premise does not hold: equal blocks."""
-    with pkg.Engine(W, W, device=0) as e:
+    with pkg.Engine(W, W, device=0, streams=2) as e:
         assert e.age_skew is None
     with pkg.Group(16640 * 2, W, 2) as grp:
         assert all(m.age_skew is None for m in grp.members)

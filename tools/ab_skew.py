@@ -27,23 +27,25 @@ def main():
     p.add_argument("--gens", type=int, default=512)
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--rule", default="ref")
+    p.add_argument("--streams", default="1", help="gol_config.streams values (0 = auto)")
     a = p.parse_args()
     pkg = entry.load_package()
     rule = pkg.REF_RULE if a.rule == "ref" else pkg.CONWAY
     for sh in a.shapes.split(","):
-        h = int(sh)
+        h, w = (int(x) for x in sh.split("x")) if "x" in sh else (int(sh), a.width)
         for ho in (int(x) for x in a.handoffs.split(",")):
             engines = []
-            for rho in a.rhos.split(","):
-                if rho == "auto":
-                    os.environ.pop("GOL_DEV_AGE_SKEW", None)
-                else:
-                    os.environ["GOL_DEV_AGE_SKEW"] = rho
-                e = pkg.Engine(h, a.width, rule=rule, device=0, handoff=ho, streams=1, resident=1)
-                e.init_random(1)
-                e.step(a.gens)  # warm-up (graph capture)
-                e.sync()
-                engines.append((rho, e, []))
+            for st in (int(x) for x in a.streams.split(",")):
+                for rho in a.rhos.split(","):
+                    if rho == "auto":
+                        os.environ.pop("GOL_DEV_AGE_SKEW", None)
+                    else:
+                        os.environ["GOL_DEV_AGE_SKEW"] = rho
+                    e = pkg.Engine(h, w, rule=rule, device=0, handoff=ho, streams=st, resident=1)
+                    e.init_random(1)
+                    e.step(a.gens)  # warm-up (graph capture)
+                    e.sync()
+                    engines.append(((rho, st), e, []))
             os.environ.pop("GOL_DEV_AGE_SKEW", None)
             for _ in range(a.rounds):
                 for rho, e, ts in engines:
@@ -59,11 +61,12 @@ def main():
                 e.sync()
                 tm = e.timing()
                 e.set_timing(0)
-                cells = float(h) * a.width * a.gens
+                cells = float(h) * w * a.gens
                 print(json.dumps({
-                    "shape": f"{h}x{a.width}", "rule": a.rule, "handoff_cfg": ho,
+                    "shape": f"{h}x{w}", "rule": a.rule, "handoff_cfg": ho,
+                    "streams_cfg": rho[1], "streams": tm.get("streams", 1),
                     "handoff": e.handoff, "tb_depth": e.tb_depth, "rows_per_wave": e.rows_per_wave,
-                    "rho": rho, "age_skew": e.age_skew, "gens": a.gens,
+                    "rho": rho[0], "age_skew": e.age_skew, "gens": a.gens,
                     "tcups_wall_median": round(cells / statistics.median(ts) / 1e12, 2),
                     "tcups_wall_best": round(cells / min(ts) / 1e12, 2),
                     "kernel_us_avg": round(tm["kernel_ms"] / max(tm["launches"], 1) * 1e3, 2),
