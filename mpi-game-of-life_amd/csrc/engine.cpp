@@ -150,7 +150,8 @@ struct RankGeom {
     std::vector<std::vector<SegDesc>> raw;
 };
 
-gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks, RankGeom* g);
+gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks, RankGeom* g,
+                         bool group = false);
 
 }  // namespace
 
@@ -656,7 +657,8 @@ gol_status check_cfg(const gol_config* cfg)
     return GOL_OK;
 }
 
-gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks, RankGeom* g)
+gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks, RankGeom* g,
+                         bool group)
 {
     gol_status st = gol_rank_rows(h, nranks, rank, &g->row0, &g->R);
     if (st != GOL_OK) return st;
@@ -692,8 +694,19 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // [R, R+Hx) (to rank+1); interior = the rest of the own rows.  Decided from
     // the smallest stripe so every rank / group member agrees (balanced stripes
     // differ by one row).
+    //
+    // Only in-process groups overlap by default.  A rank engine (one per GPU) runs
+    // one-round launches that take every wavefront slot: the band launch beside the
+    // interior launch gets slots only as interior waves retire, so it ends after
+    // the interior (a rocprofv3 trace of the 8-way rank shape: +28 us per 640 us
+    // round) and the exchange still waits for it.  Blocking exchanges after a whole
+    // last launch measured 1.3% / 2.9% / 5.7% faster per rank at 2 / 4 / 8 ranks
+    // (tools/rank_proxy.py, profiles/r02/rank_proxy_overlap.jsonl).  GOL_DEV_OVERLAP
+    // = 1 / 0 forces it on / off (dev A/B and the tests of the overlapped path).
     const int64_t Hx_ = (int64_t)g->Hx, R = (int64_t)g->R;
-    if ((int64_t)(h / (uint64_t)nranks) >= 2 * Hx_) {
+    bool want = group;
+    if (const char* ov = std::getenv("GOL_DEV_OVERLAP")) want = ov[0] == '1';
+    if ((int64_t)(h / (uint64_t)nranks) >= 2 * Hx_ && want) {
         SegDesc b = g->raw.back()[0];  // shrink Hx: out = own rows
         std::vector<SegDesc> band, inner;
         int64_t ilo = Hx_, ihi = Hx_ + R;
@@ -1383,7 +1396,7 @@ namespace {
 
 // Geometry + device state of stripe `rank` of `nranks` (no transport yet).
 gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
-                            gol_engine** out, bool shared_device = false)
+                            gol_engine** out, bool shared_device = false, bool group = false)
 {
     *out = nullptr;
     gol_status st = check_cfg(cfg);
@@ -1392,7 +1405,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
         return fail(GOL_EINVAL, "rank engines implement GLOBAL semantics only");
     if (h == 0 || w == 0) return fail(GOL_EINVAL, "h and w must be >= 1");
     RankGeom g;
-    st = rank_geometry(h, cfg, rank, nranks, &g);
+    st = rank_geometry(h, cfg, rank, nranks, &g, group);
     if (st != GOL_OK) return st;
     gol_engine* e = new (std::nothrow) gol_engine();
     if (!e) return fail(GOL_ENOMEM, "host allocation");
@@ -1488,7 +1501,7 @@ gol_status gol_create_group(uint64_t h, uint64_t w, const gol_config* cfg, int n
         c.device = devices ? devices[r] : (cfg->device >= 0 ? cfg->device : -1);
         if (std::find(devs.begin(), devs.begin() + r, devs[r]) != devs.begin() + r) c.handoff = 1;
         st = make_rank_engine(h, w, &c, r, nranks, &engines[r],
-                              std::count(devs.begin(), devs.end(), devs[r]) > 1);
+                              std::count(devs.begin(), devs.end(), devs[r]) > 1, true);
     }
     for (int r = 0; r < nranks && st == GOL_OK; ++r) {
         gol_engine* e = engines[r];

@@ -125,6 +125,7 @@ def free_port():
         return s.getsockname()[1]
 
 
+@pytest.mark.parametrize("overlap", ["default", "1"])
 @pytest.mark.parametrize("world,K,Hx,chunks,rule", [
     (2, 8, 16, (37,), "conway"),           # 2 overlapped rounds + partial
     (2, 4, 12, (12, 5, 30), "highlife"),   # overlap carried across calls
@@ -134,7 +135,13 @@ def free_port():
     (3, 7, 21, (50,), "conway"),           # remainder depths (7 = pick_depth list)
     (2, 12, 24, (24, 24, 9), "conway"),
 ])
-def test_rank_protocol_from_engine_schedule(oracle, world, K, Hx, chunks, rule):
+def test_rank_protocol_from_engine_schedule(oracle, monkeypatch, world, K, Hx, chunks, rule,
+                                            overlap):
+    """overlap: rank engines exchange blocking by default; GOL_DEV_OVERLAP=1 gives
+    the band/interior split with the overlapped exchange (inherited by the
+    spawned ranks)."""
+    if overlap != "default":
+        monkeypatch.setenv("GOL_DEV_OVERLAP", overlap)
     R = {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}[rule]
     h, w, seed = 101, 70, 5
     ctx = mp.get_context("spawn")
@@ -155,10 +162,23 @@ def test_rank_protocol_from_engine_schedule(oracle, world, K, Hx, chunks, rule):
     assert (got == ref_cells).all()
 
 
-def test_schedule_structure(pkg):
-    """The schedule's shape for the C4 8-rank stripe: 16-deep launches, a round of
-    Hx = 128 generations ending in band + interior + overlapped exchange, and the
-    next call starting from that exchange."""
+def test_schedule_structure_default(pkg):
+    """A rank engine's default schedule for the C4 8-rank stripe: rounds of Hx =
+    128 generations (eight 16-deep launches) between blocking exchanges."""
+    ops, K, Hx = pkg.round_schedule(65536, 65536, 3, 8, 300)
+    assert (K, Hx) == (16, 128)
+    kinds = [pkg.OP_NAMES[o["kind"]] for o in ops]
+    assert kinds[:18] == (["EXCHANGE"] + ["LAUNCH"] * 8) * 2
+    assert kinds[18] == "EXCHANGE" and set(kinds[19:]) == {"LAUNCH"}
+    assert "BAND" not in kinds and "EXCHANGE_ASYNC" not in kinds
+    assert sum(o["depth"] for o in ops) == 300
+
+
+def test_schedule_structure(pkg, monkeypatch):
+    """With the overlap on (GOL_DEV_OVERLAP=1; in-process groups' default): a
+    round ends in band + interior + overlapped exchange, and the next call starts
+    from that exchange."""
+    monkeypatch.setenv("GOL_DEV_OVERLAP", "1")
     ops, K, Hx = pkg.round_schedule(65536, 65536, 3, 8, 300)
     assert (K, Hx) == (16, 128)
     kinds = [pkg.OP_NAMES[o["kind"]] for o in ops]

@@ -1,7 +1,8 @@
 """The multi-rank path with more than one rank on ONE GPU: gol_create_rank_transport.
 
 RCCL refuses two ranks on one device, so these tests run the rank engines of
-gol_create_rank -- partition, halo rounds, band/interior overlap, gol_step's
+gol_create_rank -- partition, halo rounds (blocking exchanges by default, the
+band/interior overlap with GOL_DEV_OVERLAP=1), gol_step's
 schedule -- with the halo rows moved by a caller's host transport instead: here
 torch.distributed over gloo between 2-4 processes that share cuda:0 (the same
 transport shape as the reference's MPI_Sendrecv of boundary rows,
@@ -96,9 +97,15 @@ def run_ranks(world, h, w, chunks, rule, seed, **cfg):
     return res
 
 
+@pytest.mark.parametrize("overlap", ["default", "1"])
 @pytest.mark.parametrize("world,K,Hx,rule", [(2, 8, 32, "conway"), (3, 4, 16, "highlife"),
                                              (4, 16, 64, "conway"), (2, 16, 0, "ref")])
-def test_rank_engines_over_host_transport(oracle, world, K, Hx, rule):
+def test_rank_engines_over_host_transport(oracle, monkeypatch, world, K, Hx, rule, overlap):
+    """overlap: blocking exchanges (the rank engines' default) or the band /
+    interior split with the overlapped exchange (GOL_DEV_OVERLAP=1, inherited by
+    the spawned ranks)."""
+    if overlap != "default":
+        monkeypatch.setenv("GOL_DEV_OVERLAP", overlap)
     R = {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}[rule]
     h, w, seed = 1200, 2000, 11 + world
     chunks = [Hx or 128, 5, 2 * (Hx or 128) + 3, 40]  # full rounds, partial ones, carried overlap
@@ -115,9 +122,13 @@ def test_rank_engines_over_host_transport(oracle, world, K, Hx, rule):
         assert (live, hsh) == oracle.bp_digest(want, w)
 
 
-def test_rank_engines_c4_shape_over_host_transport(pkg):
-    """The C4 per-rank shape (65536^2 over 4 ranks) with default K / halo depth,
-    over 2 overlapped rounds and a partial one, equals the single field."""
+@pytest.mark.parametrize("overlap", ["default", "1"])
+def test_rank_engines_c4_shape_over_host_transport(pkg, monkeypatch, overlap):
+    """The C4 per-rank shape (65536^2 over 4 ranks) with default K / halo depth
+    (age-skewed launches), over 2 rounds and a partial one, equals the single
+    field."""
+    if overlap != "default":
+        monkeypatch.setenv("GOL_DEV_OVERLAP", overlap)
     n, world, gens = 65536, 4, 300
     with pkg.Engine(n, n, rule=pkg.CONWAY, device=0) as e:
         e.init_random(3)
