@@ -468,15 +468,23 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         return load_grp<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
     };
     // stage g (generation g+1) at step t: emits local row row_first + t - (g+1)
-    auto stage = [&](int g, int32_t t, Pl<NP> x) -> Pl<NP> {
+    // With births (rules other than B/S2) nothing may come alive outside the field:
+    // rm is the uniform row test of the emitted row (all ones or 0, a scalar), the
+    // column mask is per lane; one v_bitop3 AND3 per plane (8-byte encoding, like the
+    // rest of the hot loop).
+    auto row_mask = [&](int32_t r) -> uint32_t {  // r: field row relative to glob0 + row_first
+        return __builtin_amdgcn_readfirstlane((r >= f_lo) && (r < f_hi) ? ~0u : 0u);
+    };
+    auto stage_rm = [&](int g, Pl<NP> x, uint32_t rm) -> Pl<NP> {
         x = stage_step<RULE>(st[g], x, a.birth, a.survive);
         if constexpr (kBirths) {
-            const int32_t r = t - (g + 1);  // field row, relative to glob0 + row_first
-            const bool rok = (r >= f_lo) && (r < f_hi);
 #pragma unroll
-            for (int k = 0; k < NP; ++k) x.v[k] = rok ? (x.v[k] & cm.v[k]) : 0u;
+            for (int k = 0; k < NP; ++k) x.v[k] = lop3<kAnd3>(x.v[k], cm.v[k], rm);
         }
         return x;
+    };
+    auto stage = [&](int g, int32_t t, Pl<NP> x) -> Pl<NP> {
+        return stage_rm(g, x, kBirths ? row_mask(t - (g + 1)) : 0u);
     };
     auto store = [&](int32_t t, const Pl<NP>& x) {
         if (t >= 2 * K && t < T && st_lane)
@@ -556,6 +564,13 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         // compute, so one alignment directive places all of it; the compiler may
         // add a hazard s_nop after it, so the 4-byte pad that gives the wanted
         // parity is per kernel: loop_place.h, generated by tools/loop_align.py.
+        // the block's row masks, computed ahead of the compute (scalar code stays out
+        // of the placed region): stage g at step t0 + p emits row t0 + p - g - 1
+        uint32_t rmv[kPrefetch + K - 1];
+        if constexpr (kBirths) {
+#pragma unroll
+            for (int j = 0; j < kPrefetch + K - 1; ++j) rmv[j] = row_mask(t0 - K + j);
+        }
         if constexpr (!kGuard) {
             __builtin_amdgcn_sched_barrier(0);
             place_block<life_loop_pad(K, RULE, NP, HAND, TOFF) != 0, NP, kPrefetch>(x);
@@ -570,7 +585,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
             for (int p = 0; p < kPrefetch; ++p) {
                 const int g = d - p;
                 if (g >= 0 && g < K && (!kGuard || t0 + p >= 2 * g)) {
-                    x[p] = stage(g, t0 + p, x[p]);
+                    x[p] = stage_rm(g, x[p], kBirths ? rmv[p - g - 1 + K] : 0u);
                     if constexpr (HAND && kGuard && !(GOL_EXP & 4)) {
                         if (g <= K - 2 && (t0 + p == 2 * g + 2 || t0 + p == 2 * g + 3))
                             store_side<NP>(reinterpret_cast<uint64_t*>(
