@@ -395,11 +395,10 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
 // 33024; profiles/r02/wave_log_*.jsonl).  Balancing the pair by priority instead
 // (s_setprio flips, closed loop) was measured 9-10% slower.  So the older units
 // get longer blocks: the bottom blocks of each strip whose units are < units_old
-// have rows_old rows, the others R, with the young/old rate ratio kAgeRate fitted
-// to the pairs' end stamps; the block count, and so the units, stay as planned.
-// Returns rows_old (0 = no skew).  GOL_DEV_AGE_SKEW overrides kAgeRate (dev A/B;
-// 0 turns the skew off).
-constexpr double kAgeRate = 0.78;
+// have rows_old rows, the others rows_young, with the young/old rate ratio rho of
+// the block kind (kAgeRate*; the in-process A/B optimum, profiles/r02/ab_skew*.jsonl).
+// GOL_DEV_AGE_SKEW overrides rho (dev A/B; 0 turns the skew off).
+constexpr double kAgeRateHand = 0.78, kAgeRateClassic = 0.72;
 
 constexpr double kHandSkewCost = 1.05;
 
@@ -412,9 +411,7 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
               int planes, bool hand)
 {
     Skew best_s;
-    // young/old issue-rate ratio of a SIMD's pair (end-stamp fit; the in-process
-    // A/B optimum, profiles/r02/ab_skew.jsonl)
-    double rho = hand ? 0.78 : 0.72;
+    double rho = hand ? kAgeRateHand : kAgeRateClassic;
     if (const char* v = std::getenv("GOL_DEV_AGE_SKEW")) rho = std::atof(v);
     const int64_t rows = sg.out_hi - sg.out_lo;
     if (rho <= 0 || rho >= 1 || occ != 2 || rows <= 0) return best_s;
