@@ -80,3 +80,28 @@ def test_no_skew_for_forced_rows_or_multi_round(pkg):
         assert e.age_skew is None  # a caller's rows_per_wave is kept as given
     with pkg.Engine(2048, W, device=0, streams=1, resident=1) as e:
         assert e.age_skew is None  # fewer units than one workgroup per CU x 4
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+@pytest.mark.parametrize("h,w,skewed", [
+    (9000, 20000, True),     # 6 strips, blocks of 35 / 19 rows
+    (12001, 65613, True),    # odd height, a partial last lane group, hand-off blocks
+    (7001, 40000, True),     # 11 strips, a partial 11th
+    (6500, 65536, True),     # the shortest stripe at K = 16, hand-off
+    (20000, 3000, False),    # one strip at the minimum block length: nothing to skew
+    (5003, 65613, False),    # K = 8 (more than 2 waves per SIMD): equal blocks
+])
+def test_skew_shapes_vs_oracle(pkg, oracle, h, w, skewed, rule):
+    """Skewed launches on shapes away from the bench's: a few strips, odd widths
+    and heights (a partial last lane group and last block), both block kinds, and
+    shapes the planner leaves unskewed -- 27 generations (full-depth launches and
+    the remainder depths)."""
+    R = rule_of(oracle, rule)
+    gens = 16 + 8 + 3
+    with pkg.Engine(h, w, rule=R, device=0, streams=1, resident=1) as e:
+        assert (e.age_skew is not None) == skewed, e.age_skew
+        e.init_random(11)
+        e.step(gens)
+        got = e.digest()
+    g = oracle.bp_run(oracle.bp_random(h, w, 11), w, gens, R, threads=THREADS)
+    assert got == oracle.bp_digest(g, w)
