@@ -166,6 +166,38 @@ def cpu_baseline(w, seed, threads=0):
     return rec
 
 
+def rccl_selfcheck(pkg, dist, torch, world, rank, local):
+    """N > 1: the RCCL halo path end to end on a small field before the timed run.
+    Every rank advances its stripe of a 4096^2 B3/S23 field (rounds of Hx
+    generations with ncclSend/Recv exchanges) and the stripe digests are summed
+    (digests are order-independent sums, engine.cpp digest_kernel); rank 0 evolves
+    the whole field alone on its GPU and compares.  Not part of the timed region."""
+    n, gens, seed = 4096, 3 * 64 + 21, 5
+    uid = [pkg.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    with pkg.Engine(n, n, rule=pkg.CONWAY, device=local, rank=rank, nranks=world,
+                    uid=uid[0]) as e:
+        hx = e.halo_depth
+        e.init_random(seed)
+        e.step(gens)
+        live, hsh = e.digest()
+    mask = (1 << 64) - 1
+    t = torch.tensor([live, hsh - (1 << 64) if hsh >= (1 << 63) else hsh], dtype=torch.int64,
+                     device="cuda")
+    dist.all_reduce(t)  # int64 sums wrap mod 2^64 like the digest's
+    got = (int(t[0].item()) & mask, int(t[1].item()) & mask)
+    rec = {"field": f"{n}x{n}", "rule": "B3/S23", "generations": gens, "halo_depth": hx,
+           "ranks": world}
+    if rank == 0:
+        with pkg.Engine(n, n, rule=pkg.CONWAY, device=local) as ref:
+            ref.init_random(seed)
+            ref.step(gens)
+            want = ref.digest()
+        rec["ok"] = got == want
+        rec["digest"] = list(got)
+    return rec
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,8 +222,10 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         eng = pkg.Engine(n, n, halo_depth=a.halo_depth, rank=rank, nranks=world, uid=uid[0],
                          **kw)
+        selfcheck = rccl_selfcheck(pkg, dist, torch, world, rank, local)
     else:
         eng = pkg.Engine(n, n, streams=a.streams, **kw)
+        selfcheck = None
     eng.init_random(a.seed)
 
     def barrier():
@@ -309,6 +343,7 @@ def main():
                                             / (HBM_PEAK_GBPS * 1e9), 4) if traffic else None),
             },
             "cpu_baseline": None,
+            "rccl_selfcheck": selfcheck,
         }
         if world == 1 and not a.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(n, a.seed, a.cpu_threads)
