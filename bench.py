@@ -313,6 +313,7 @@ def main():
                 "tb_depth": eng.tb_depth, "word_planes": eng.word_planes,
                 "halo_depth": eng.halo_depth, "rows_per_wave": eng.rows_per_wave,
                 "handoff": eng.handoff, "resident": eng.resident,
+                "age_skew": eng.age_skew,
                 "parallelism": f"row-stripes x{world}" if world > 1 else "single GPU",
             },
             "roofline": {

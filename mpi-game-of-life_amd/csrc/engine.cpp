@@ -408,7 +408,7 @@ struct Skew {
 };
 
 Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, int occ, int K,
-              int planes, bool hand)
+              int planes, bool hand, int64_t max_units = INT64_MAX)
 {
     Skew best_s;
     double rho = hand ? kAgeRateHand : kAgeRateClassic;
@@ -423,20 +423,25 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
     const int64_t nb0 = (rows + R - 1) / R;
     const double nw = std::ceil((double)(nb0 * strips) / (double)units_old);
     double best = std::max(0.0, nw - 2) * cost(R) / (1 + rho) + cost(R) / rho;
+    // Lengths step: hand-off blocks keep both lengths in one class mod the
+    // prefetch block (one tail offset per launch: R or R + pf/2), classic ones
+    // take any length.
+    const int step = hand ? pf : 1;
     // every block count of one round of more than units_old (= one per SIMD)
     // wavefronts: the old blocks from the mean length to twice it
-    for (int64_t nblk = std::max<int64_t>(2, units_old / strips + 1); nblk * strips <= 2 * units_old;
-         ++nblk) {
+    for (int64_t nblk = std::max<int64_t>(2, units_old / strips + 1);
+         nblk * strips <= std::min(2 * units_old, max_units); ++nblk) {
         const int64_t units = nblk * strips;
         if (units <= units_old) continue;
         const int64_t mean = (rows + nblk - 1) / nblk;
-        const int64_t ro0 = mean + ((R - mean) % pf + pf) % pf;
         auto jold = [&](int64_t s) {
             return std::min<int64_t>(nblk, std::max<int64_t>(0, (units_old - s + strips - 1) / strips));
         };
-        for (int64_t ro = ro0; ro <= 2 * mean + pf; ro += pf) {
-            // the young length: the least in ro's class mod pf (= R's, so the launch
-            // keeps R's hand-off tail offset) that covers every strip
+        for (int cls = 0; cls < (hand ? 2 : 1); ++cls)
+        for (int64_t ro = mean + ((R + cls * pf / 2 - mean) % step + step) % step;
+             ro <= 2 * mean + pf; ro += step) {
+            // the young length: the least in ro's class mod step that covers every
+            // strip
             int64_t ry = 1;
             bool ok = true;
             for (int64_t s = 0; s < strips && ok; ++s) {
@@ -447,7 +452,7 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
                     ry = std::max<int64_t>(ry, (rows - jo * ro + ny - 1) / ny);
             }
             if (!ok) continue;
-            ry += ((ro - ry) % pf + pf) % pf;
+            ry += ((ro - ry) % step + step) % step;
             if (ry >= ro || !fits(ry) || !fits(ro)) continue;
             // every strip's blocks cover the rows and its last block is not empty
             for (int64_t s = 0; s < strips && ok; ++s) {
@@ -559,6 +564,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         // the band launch runs beside the interior launch: classic blocks, so that
         // at most one launch that waits for its own wavefronts runs at a time
         const bool band = e->overlap && pi == (size_t)e->Hx;
+        const bool inner = e->overlap && pi == (size_t)e->Hx + 1;
         const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
                                               (int)e->rows_per_wave, e->lane_shift,
                                               band ? 1u : handoff);
@@ -566,19 +572,53 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         p.groups = rp.groups;
         p.lane_shift = rp.lane_shift;
         p.hand = rp.hand;
+        // Overlapped rounds (rank engines / groups alone on their device): the band
+        // launch must find free wavefront slots beside the interior launch, or it
+        // runs after it and the exchange waits.  The band's blocks are
+        // sized so that its single waves end well inside the interior launch (about
+        // 60% of the full launch's per-wave cost, at the young rate), and the
+        // interior launch leaves the band's slots free.
+        const int64_t slots_first = (int64_t)gol::kWavesPerBlock * cus;  // one workgroup per CU
+        if (band && !e->rows_per_wave && !e->shared_device && e->Hx >= 1) {
+            const auto& full = e->plans[e->Hx - 1];
+            const double cf = full.hand ? 1.02 * (double)full.rpw + 10.0
+                                        : (double)(full.rpw + e->K + 4);
+            const int64_t rb = (int64_t)(0.6 * cf * kAgeRateClassic) - (int64_t)e->K - 4;
+            p.rpw = std::max<int64_t>(std::max<int64_t>(8, e->K + 2), std::min<int64_t>(rb, (int64_t)e->Hx));
+            p.hand = false;
+        }
         finish_segs(p.segs, p.rpw, p.groups);
         p.total_units = plan_units(p.segs, p.groups);
+        int64_t cap = INT64_MAX;
+        if (inner && !e->rows_per_wave && !e->shared_device) {
+            const int occ = p.hand ? occ_h : occ_c;
+            cap = (int64_t)occ * slots_first - e->plans[e->Hx].total_units;
+            if (cap > slots_first && p.total_units > cap) {
+                int64_t R = p.rpw;
+                std::vector<SegDesc> segs = p.segs;
+                do {
+                    ++R;
+                    if (p.hand && !handoff_fits(R, (int)e->K, e->planes)) continue;
+                    finish_segs(segs, R, p.groups);
+                } while (plan_units(segs, p.groups) > cap && R < 4096);
+                p.rpw = R;
+                p.segs = segs;
+                p.total_units = plan_units(p.segs, p.groups);
+            }
+        }
         if (!band && p.segs.size() == 1 && !e->rows_per_wave && !e->shared_device) {
             const int occ = p.hand ? occ_h : occ_c;
-            const int64_t first = (int64_t)gol::kWavesPerBlock * cus;  // one workgroup per CU
+            const int64_t first = slots_first;
             const Skew sk = age_skew(p.segs[0], p.rpw, p.groups, first, occ, (int)e->K,
-                                     e->planes, p.hand);
+                                     e->planes, p.hand, cap);
             if (sk.rows_old) {
                 p.rows_young = (int32_t)sk.rows_young;
                 p.rows_old = (int32_t)sk.rows_old;
                 p.units_old = (int32_t)first;
                 p.segs[0].nblk = sk.nblk;
                 p.total_units = plan_units(p.segs, p.groups);
+                // the launch's hand-off tail offset follows the lengths' class
+                p.rpw = sk.rows_young;
             }
         }
         for (const auto& sg : p.segs) {
@@ -601,6 +641,11 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         }
         max_units = std::max(max_units, p.total_units);
         any_hand |= p.hand && p.multi_blk;
+        if (std::getenv("GOL_DEV_PLANS"))  // dev: the launch plans as built
+            std::fprintf(stderr, "plan %zu: rows [%lld, %lld) x %zu segs, R %lld, strips %d, units %lld, "
+                         "hand %d, skew %d/%d\n", pi, (long long)p.segs[0].out_lo,
+                         (long long)p.segs[0].out_hi, p.segs.size(), (long long)p.rpw, p.groups,
+                         (long long)p.total_units, (int)p.hand, p.rows_old, p.rows_young);
         HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * p.segs.size()));
         HIP_TRY(hipMemcpy(p.dev, p.segs.data(), sizeof(SegDesc) * p.segs.size(),
                           hipMemcpyHostToDevice));
@@ -693,13 +738,17 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // differ by one row).
     //
     // Only in-process groups overlap by default.  A rank engine (one per GPU) runs
-    // one-round launches that take every wavefront slot: the band launch beside the
-    // interior launch gets slots only as interior waves retire, so it ends after
-    // the interior (a rocprofv3 trace of the 8-way rank shape: +28 us per 640 us
-    // round) and the exchange still waits for it.  Blocking exchanges after a whole
-    // last launch measured 1.3% / 2.9% / 5.7% faster per rank at 2 / 4 / 8 ranks
-    // (tools/rank_proxy.py, profiles/r02/rank_proxy_overlap.jsonl).  GOL_DEV_OVERLAP
-    // = 1 / 0 forces it on / off (dev A/B and the tests of the overlapped path).
+    // one-round launches that take every wavefront slot: a band launch beside the
+    // interior launch gets slots only as interior waves retire, ends after the
+    // interior and the exchange waits for it (rocprofv3 trace of one 8-way rank:
+    // +28 us per 640 us round, profiles/r02/trace_rank8_overlap_kernels.csv);
+    // blocking exchanges were 1.3-5.7% faster per rank.  With the planner's cap
+    // (band blocks sized to end early, the interior launch leaving their slots free,
+    // build_plans) the band does run concurrently (trace_rank8_overlap_capped.csv),
+    // but per-rank rates through the host-transport proxy stayed within -3..+3% of
+    // blocking and bimodal at 2 ranks, and an RCCL exchange is itself a kernel that
+    // needs free slots: blocking stays the rank default.  GOL_DEV_OVERLAP = 1 / 0
+    // forces the overlap on / off (dev A/B and the tests of both paths).
     const int64_t Hx_ = (int64_t)g->Hx, R = (int64_t)g->R;
     bool want = group;
     if (const char* ov = std::getenv("GOL_DEV_OVERLAP")) want = ov[0] == '1';
