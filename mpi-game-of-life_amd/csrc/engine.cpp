@@ -609,8 +609,29 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         if (!band && p.segs.size() == 1 && !e->rows_per_wave && !e->shared_device) {
             const int occ = p.hand ? occ_h : occ_c;
             const int64_t first = slots_first;
-            const Skew sk = age_skew(p.segs[0], p.rpw, p.groups, first, occ, (int)e->K,
-                                     e->planes, p.hand, cap);
+            Skew sk = age_skew(p.segs[0], p.rpw, p.groups, first, occ, (int)e->K, e->planes,
+                               p.hand, cap);
+            // Auto block kind, per plan: hand-off lengths are confined to two classes
+            // mod the prefetch block, which can leave a launch without a close
+            // one-round fit (8416 rows in 113 blocks of 86/62 rows: 90 vs 77 us); a
+            // skewed classic plan is taken when the model says it is faster.
+            if (p.hand && e->handoff == 0) {
+                const RowPlan rc = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h,
+                                                      4 * cus, 0, e->lane_shift, 1u);
+                std::vector<SegDesc> cs = r;
+                finish_segs(cs, rc.rpw, rc.groups);
+                const Skew skc = age_skew(cs[0], rc.rpw, rc.groups, first, occ_c, (int)e->K,
+                                          e->planes, false, cap);
+                if (!rc.hand && skc.rows_old &&
+                    (!sk.rows_old || skc.t < sk.t * kHandSkewCost)) {
+                    p.hand = false;
+                    p.rpw = rc.rpw;
+                    p.groups = rc.groups;
+                    p.lane_shift = rc.lane_shift;
+                    p.segs = cs;
+                    sk = skc;
+                }
+            }
             if (sk.rows_old) {
                 p.rows_young = (int32_t)sk.rows_young;
                 p.rows_old = (int32_t)sk.rows_old;
