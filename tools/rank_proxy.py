@@ -47,9 +47,9 @@ def noop_transport(pkg):
     return pkg.Transport(fn, None), (lib, fn)
 
 
-def rank_engine(pkg, n, rank, nranks, tp):
+def rank_engine(pkg, n, rank, nranks, tp, handoff=0):
     import ctypes
-    cfg = pkg.make_config(pkg.REF_RULE, 0, pkg.SEM_GLOBAL, 1, 0, 0, 0, 0, 0, 0, 0, 0)
+    cfg = pkg.make_config(pkg.REF_RULE, 0, pkg.SEM_GLOBAL, 1, 0, 0, 0, handoff, 0, 0, 0, 0)
     h = ctypes.c_void_p()
     pkg._check(pkg.lib().gol_create_rank_transport(n, n, ctypes.byref(cfg), rank, nranks,
                                                    ctypes.byref(tp), ctypes.byref(h)))
@@ -63,6 +63,7 @@ def main():
     p.add_argument("--skews", default="auto,0", help="GOL_DEV_AGE_SKEW values (auto = unset)")
     p.add_argument("--gens", type=int, default=1000)
     p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--handoff", type=int, default=0, help="gol_config.handoff")
     p.add_argument("--overlaps", default="default", help="GOL_DEV_OVERLAP values (default = unset)")
     a = p.parse_args()
     pkg = entry.load_package()
@@ -81,7 +82,7 @@ def main():
                     os.environ.pop("GOL_DEV_OVERLAP", None)
                 else:
                     os.environ["GOL_DEV_OVERLAP"] = ov
-                e = rank_engine(pkg, n, rank, N, tp)
+                e = rank_engine(pkg, n, rank, N, tp, a.handoff)
                 e.init_random(1)
                 e.step(a.gens)
                 e.sync()
