@@ -437,9 +437,12 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
         auto jold = [&](int64_t s) {
             return std::min<int64_t>(nblk, std::max<int64_t>(0, (units_old - s + strips - 1) / strips));
         };
+        // at most ~256 old lengths per block count (long blocks step coarser), so
+        // that plan building stays fast for tall fields and many rank plans
+        const int64_t stride = step * std::max<int64_t>(1, mean / (256 * step));
         for (int cls = 0; cls < (hand ? 2 : 1); ++cls)
         for (int64_t ro = mean + ((R + cls * pf / 2 - mean) % step + step) % step;
-             ro <= 2 * mean + pf; ro += step) {
+             ro <= 2 * mean + pf; ro += stride) {
             // the young length: the least in ro's class mod step that covers every
             // strip
             int64_t ry = 1;
