@@ -90,13 +90,20 @@ def valu_peak_rate():
 
 
 def counters_for(cfg):
-    """Per-launch PMC record (SQ_INSTS_VALU, HBM bytes) of this configuration."""
+    """Per-launch PMC record (SQ_INSTS_VALU, HBM bytes) of this configuration: the
+    record with the same field, rule, depth, streams, GPUs and block kind whose
+    rows per wavefront is the same or within 2% (a plan a row or two different
+    moves the counters by well under 1%)."""
     rec = load_json("profiles/r02/counters.json") or {}
+    keys = ("size", "rule", "tb_depth", "streams", "n_gpus", "handoff")
+    best = None
     for r in rec.get("records", []):
-        if all(r.get(k) == cfg.get(k) for k in ("size", "rule", "tb_depth", "streams", "n_gpus",
-                                                "rows_per_wave", "handoff")):
-            return r
-    return None
+        if not all(r.get(k) == cfg.get(k) for k in keys):
+            continue
+        d = abs(r.get("rows_per_wave", 0) - cfg.get("rows_per_wave", 0))
+        if d <= 0.02 * max(1, cfg.get("rows_per_wave", 0)) and (best is None or d < best[0]):
+            best = (d, r)
+    return best[1] if best else None
 
 
 def host_info():
@@ -337,7 +344,8 @@ def main():
                                    if insts else None),
                     "peak_from": "profiles/r01/valu_rate.json (v_bitop3, 2 waves/SIMD, best "
                                  "code placement) x 1024 SIMDs",
-                    "counters_from": "profiles/r02/counters.json" if insts else None,
+                    "counters_from": (f"profiles/r02/counters.json (record of rows_per_wave "
+                                      f"{ctr.get('rows_per_wave')})" if insts else None),
                 },
                 "hbm_equiv_frac": round(BYTES_PER_CELL_GEN * gcups / HBM_PEAK_GBPS, 4),
                 "hbm_measured_frac": (round(traffic * streams / launch_s
