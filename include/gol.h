@@ -167,8 +167,9 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0,
                     uint32_t* rows_per_wave);
 
 /* Launch plan of a full-depth launch as chosen (strip width in lanes, rows per
- * wavefront, planes per lane); a composite engine reports its first stripe's
- * plan.  Any out pointer may be NULL. */
+ * wavefront, planes per lane); with age-skewed blocks the rows per wavefront are
+ * the shorter (young) length, gol_plan_skew gives both.  A composite engine
+ * reports its first stripe's plan.  Any out pointer may be NULL. */
 gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave,
                          uint32_t* word_planes);
 
