@@ -133,30 +133,46 @@ def host_info():
     except Exception:
         cc = "gcc"
     return {"cpu_model": model, "cpus_allowed": len(allowed), "physical_cores": len(cores),
-            "compiler": cc + ", -O2 -fPIC (oracle/Makefile)"}
+            "compiler": cc + ", -O3 -fPIC (oracle/Makefile)"}
 
 
 def cpu_baseline(w, seed, threads=0):
     """Oracle port of the reference algorithm (int per cell, per-cell neighbour
     loop) on the benchmark's own field: `threads` stripes of 512 rows x w columns
     (rows [0, threads*512) of the splitmix64 field), each evolved alone like one
-    `mpirun -np threads` rank, E = 64 generations of B/S2; GCUPS from
-    T(E) - T(0), so building the field is not counted."""
+    `mpirun -np threads` rank (Parallel_Life_MPI.cpp:199, :215-221, :233-237).
+    Two samples, GCUPS from T(E) - T(0) so building the field is not counted:
+    E = 160 generations of B/S2 (`value`: the field is p = 0.5 for ~3 generations,
+    then sparse, like the GPU run's 1000) and E = 3 on stripes of 2048 rows
+    (`dense`: the p = 0.5 regime only)."""
     info = host_info()
+    capped = None
     if not threads:
-        threads = info["cpus_allowed"]
+        threads = info["physical_cores"]
         omp = os.environ.get("OMP_NUM_THREADS")
-        if omp and omp.isdigit():  # the box's CPU share (set there)
-            threads = min(threads, int(omp))
+        if omp and omp.isdigit() and int(omp) < threads:
+            # the GPU pool gives one GPU's job a CPU share of OMP_NUM_THREADS
+            # threads (16) of the host's cores and asks worker pools to stay in it
+            capped = (f"{int(omp)} of {threads} physical cores: the GPU box's CPU share for "
+                      f"a one-GPU job (OMP_NUM_THREADS={omp}; the pool asks worker pools to "
+                      f"stay within it)")
+            threads = int(omp)
     orc = entry.load_oracle()
-    rows, gens = 512, 64
-    t0 = time.perf_counter()
-    orc.ref_baseline(rows, w, 0, threads, seed)
-    t_init = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    orc.ref_baseline(rows, w, gens, threads, seed)
-    t = time.perf_counter() - t0 - t_init
-    gcups = threads * rows * w * gens / t / 1e9
+    rows = 512
+
+    def rate(rows, gens):
+        t0 = time.perf_counter()
+        orc.ref_baseline(rows, w, 0, threads, seed)
+        t_init = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        orc.ref_baseline(rows, w, gens, threads, seed)
+        t = time.perf_counter() - t0 - t_init
+        return threads * rows * w * gens / t / 1e9, t
+
+    # about 13 s and 3 s of CPU work on the box (16 EPYC 9575F cores)
+    sparse_gens, dense_rows = 160, 2048
+    gcups, t = rate(rows, sparse_gens)
+    dense, td = rate(dense_rows, 3)
     rec = {
         "value": round(gcups, 4),
         "unit": "GCUPS",
@@ -165,12 +181,23 @@ def cpu_baseline(w, seed, threads=0):
         "why_port": "the reference binary is unbuildable here: Parallel_Life_MPI.cpp:6 "
                     "includes <windows.h>",
         "sample": f"{threads} stripes x {rows} rows x {w} cols of the bench field (splitmix64 "
-                  f"seed {seed}), E = {gens} generations of B/S2 (dense for ~3 generations, "
+                  f"seed {seed}), E = {sparse_gens} generations of B/S2 (dense for ~3 generations, "
                   f"then sparse), T(E) - T(0) = {t:.2f} s",
         "per_core_mcups": round(gcups * 1e3 / threads, 1),
+        "dense": {"value": round(dense, 4), "unit": "GCUPS",
+                  "per_core_mcups": round(dense * 1e3 / threads, 1),
+                  "sample": f"{threads} stripes x {dense_rows} rows x {w} cols of the same field, "
+                            f"E = 3 generations (p = 0.5 throughout), "
+                            f"T(E) - T(0) = {td:.2f} s"},
+        "cores_capped": capped,
     }
     rec.update(info)
     return rec
+
+
+def ctl_device(dist):
+    """Device of the control-plane tensors (timing max, digest sums)."""
+    return "cpu" if dist.get_backend() == "gloo" else "cuda"
 
 
 def rccl_selfcheck(pkg, dist, torch, world, rank, local):
@@ -190,7 +217,7 @@ def rccl_selfcheck(pkg, dist, torch, world, rank, local):
         live, hsh = e.digest()
     mask = (1 << 64) - 1
     t = torch.tensor([live, hsh - (1 << 64) if hsh >= (1 << 63) else hsh], dtype=torch.int64,
-                     device="cuda")
+                     device=ctl_device(dist))
     dist.all_reduce(t)  # int64 sums wrap mod 2^64 like the digest's
     got = (int(t[0].item()) & mask, int(t[1].item()) & mask)
     rec = {"field": f"{n}x{n}", "rule": "B3/S23", "generations": gens, "halo_depth": hx,
@@ -210,6 +237,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GOL_DEV_RCCL_SELF=1 (rehearsal of the N > 1 path on a one-GPU box): every
+    # rank's engine talks RCCL to itself (engine.cpp gol_create_rank), ranks share
+    # the GPUs there are, torch.distributed runs over gloo (RCCL refuses two ranks
+    # of one communicator on one device), and rccl_selfcheck is expected to fail
+    # (a self-looped stripe is not the field's stripe)
+    rehearsal = os.environ.get("GOL_DEV_RCCL_SELF") == "1"
     if world != a.gpus:
         if not (world == 1 and a.gpus == 1):
             raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch with torchrun")
@@ -220,24 +253,54 @@ def main():
     pkg = entry.load_package()
     rule = pkg.REF_RULE if a.rule == "ref" else pkg.CONWAY
     n = a.size
+    if rehearsal:
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     kw = dict(rule=rule, device=local, tb_depth=a.tb_depth, rows_per_wave=a.rows_per_wave,
               handoff=a.handoff)
-    if world > 1:
-        dist.init_process_group("nccl")
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def rank_engine(overlap):
         uid = [pkg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        eng = pkg.Engine(n, n, halo_depth=a.halo_depth, rank=rank, nranks=world, uid=uid[0],
-                         **kw)
+        return pkg.Engine(n, n, halo_depth=a.halo_depth, rank=rank, nranks=world, uid=uid[0],
+                          exchange_overlap=overlap, **kw)
+
+    modes = None
+    if world > 1:
+        dist.init_process_group("gloo" if rehearsal else "nccl")
         selfcheck = rccl_selfcheck(pkg, dist, torch, world, rank, local)
+        # the overlapped exchange (band launch + RCCL exchange on a side stream
+        # beside the interior launch, exchange_overlap = 2) against the default
+        # blocking one: the same K steps, reported beside `value`
+        eng = rank_engine(2)
+        eng.init_random(a.seed)
+        for _ in range(a.warmup):
+            eng.step(a.gens)
+        eng.sync()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            eng.step(a.gens)
+        eng.sync()
+        torch.cuda.synchronize()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                         device=ctl_device(dist))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ov_dt = float(t.item())
+        eng.close()
+        modes = {"overlapped": {"value": round(float(n) * n * a.gens * a.steps / ov_dt / 1e9, 2),
+                                "ms_per_step": round(ov_dt / a.steps * 1e3, 3),
+                                "halo_depth": None}}
+        eng = rank_engine(0)
     else:
         eng = pkg.Engine(n, n, streams=a.streams, **kw)
         selfcheck = None
     eng.init_random(a.seed)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
 
     for _ in range(a.warmup):
         eng.step(a.gens)
@@ -271,11 +334,11 @@ def main():
         dt_graph = min(dt_graph, time.perf_counter() - t1)
     barrier()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=ctl_device(dist))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         k = torch.tensor([tm["kernel_ms"] / max(tm["launches"], 1)], dtype=torch.float64,
-                         device="cuda")
+                         device=ctl_device(dist))
         dist.all_reduce(k, op=dist.ReduceOp.MAX)
         avg_launch_ms = float(k.item())
     else:
@@ -283,6 +346,11 @@ def main():
 
     cell_gens = float(n) * n * a.gens * a.steps
     gcups = cell_gens / dt / 1e9
+    if modes is not None:
+        modes["blocking"] = {"value": round(gcups, 2), "ms_per_step": round(dt / a.steps * 1e3, 3),
+                             "halo_depth": eng.halo_depth, "default": True}
+        modes["overlapped"]["halo_depth"] = eng.halo_depth
+    ok = selfcheck is None or selfcheck.get("ok", True)
     # dominant kernel: the fused stencil (HIP events on each stripe's stream)
     cg_per_launch = tm["cell_gens"] / max(tm["launches"], 1)
     # a composite engine (gol_config.streams > 1) runs that many stripe launches
@@ -301,7 +369,8 @@ def main():
     if rank == 0:
         rec = {
             "metric": METRIC,
-            "value": round(gcups, 2),
+            # a failed RCCL self-check voids the multi-GPU number
+            "value": round(gcups, 2) if (ok or rehearsal) else None,
             "unit": "GCUPS",
             "n_gpus": world,
             "steps": a.steps,
@@ -353,6 +422,7 @@ def main():
             },
             "cpu_baseline": None,
             "rccl_selfcheck": selfcheck,
+            "exchange_modes": modes,
         }
         if world == 1 and not a.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(n, a.seed, a.cpu_threads)
@@ -360,6 +430,10 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+    if rank == 0 and not ok and not rehearsal:
+        print("rccl_selfcheck failed: the RCCL halo path does not reproduce the single "
+              "field", file=sys.stderr)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

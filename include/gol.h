@@ -99,6 +99,15 @@ typedef struct gol_config {
                               word_planes -- is set), 1 = off, 2 = on if the
                               field fits (then tb_depth sets K and rows_per_wave
                               the rows each wavefront holds: 2,3,4,6,8) */
+    uint32_t exchange_overlap; /* rank engines and groups: 0 = auto (rank engines
+                              exchange after the round's last launch, blocking;
+                              in-process groups overlap), 1 = blocking, 2 =
+                              overlapped (the round's last launch splits into a
+                              band launch of the rows the neighbours need and an
+                              interior launch, and the exchange of the band rows
+                              runs on a side stream beside the interior launch;
+                              needs stripes of >= 2 halo_depth rows, else
+                              blocking) */
 } gol_config;
 
 typedef struct gol_engine gol_engine;

@@ -59,6 +59,7 @@ class Config(ctypes.Structure):
         ("strip_lanes", ctypes.c_uint32),
         ("word_planes", ctypes.c_uint32),
         ("resident", ctypes.c_uint32),
+        ("exchange_overlap", ctypes.c_uint32),
     ]
 
 
@@ -174,7 +175,7 @@ def _check(st):
 
 def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_depth=0,
                 halo_depth=0, rows_per_wave=0, handoff=0, streams=0, strip_lanes=0,
-                word_planes=0, resident=0):
+                word_planes=0, resident=0, exchange_overlap=0):
     c = Config()
     lib().gol_config_init(ctypes.byref(c))
     c.birth_mask, c.survive_mask = rule
@@ -189,6 +190,7 @@ def make_config(rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1, tb_
     c.strip_lanes = strip_lanes
     c.word_planes = word_planes
     c.resident = resident
+    c.exchange_overlap = exchange_overlap
     return c
 
 
@@ -229,7 +231,7 @@ class Engine:
     def __init__(self, h, w, rule=REF_RULE, device=-1, semantics=SEM_GLOBAL, ref_ranks=1,
                  tb_depth=0, halo_depth=0, rows_per_wave=0, rank=None, nranks=1, uid=None,
                  handoff=0, streams=0, strip_lanes=0, word_planes=0, transport=None,
-                 resident=0, _handle=None):
+                 resident=0, exchange_overlap=0, _handle=None):
         """transport: for a rank engine, a callable (send_up, send_down) -> (recv_up,
         recv_down) of bytes objects (None where there is no neighbour) used instead
         of RCCL (gol_create_rank_transport)."""
@@ -237,7 +239,8 @@ class Engine:
         self.wq = (w + 63) // 64
         self._tp = None
         cfg = make_config(rule, device, semantics, ref_ranks, tb_depth, halo_depth,
-                          rows_per_wave, handoff, streams, strip_lanes, word_planes, resident)
+                          rows_per_wave, handoff, streams, strip_lanes, word_planes, resident,
+                          exchange_overlap)
         handle = ctypes.c_void_p()
         if _handle is not None:
             handle = _handle
@@ -371,11 +374,11 @@ class Group:
     share a GPU."""
 
     def __init__(self, h, w, nranks, devices=None, rule=REF_RULE, tb_depth=0, halo_depth=0,
-                 rows_per_wave=0, handoff=0, strip_lanes=0, word_planes=0):
+                 rows_per_wave=0, handoff=0, strip_lanes=0, word_planes=0, exchange_overlap=0):
         self.h, self.w, self.n = h, w, nranks
         cfg = make_config(rule, -1 if devices else 0, SEM_GLOBAL, 1, tb_depth, halo_depth,
                           rows_per_wave, handoff, strip_lanes=strip_lanes,
-                          word_planes=word_planes)
+                          word_planes=word_planes, exchange_overlap=exchange_overlap)
         hs = (ctypes.c_void_p * nranks)()
         devs = (ctypes.c_int * nranks)(*(devices or [0] * nranks))
         _check(lib().gol_create_group(h, w, ctypes.byref(cfg), nranks, devs, hs))

@@ -180,6 +180,9 @@ struct gol_engine {
     uint64_t row0 = 0, R = 0, Hx = 0;
     XferKind xfer = XFER_NONE;
     ncclComm_t comm = nullptr;
+    // RCCL peers of the up/down halo (rank -+ 1; both 0 for the self-loop test
+    // communicator of GOL_DEV_RCCL_SELF, gol_create_rank)
+    int peer_up = -1, peer_dn = -1;
     gol_transport tp{nullptr, nullptr};
     uint64_t* host_xfer = nullptr;  // pinned: send_up | recv_up | send_dn | recv_dn
 
@@ -714,6 +717,8 @@ gol_status check_cfg(const gol_config* cfg)
         return fail(GOL_EINVAL, "strip_lanes must be 0 (auto), 64, 32 or 16");
     if (cfg->semantics > GOL_SEM_REF_STRIPES) return fail(GOL_EINVAL, "bad semantics");
     if (cfg->resident > 2) return fail(GOL_EINVAL, "resident must be 0 (auto), 1 (off) or 2 (on)");
+    if (cfg->exchange_overlap > 2)
+        return fail(GOL_EINVAL, "exchange_overlap must be 0 (auto), 1 (blocking) or 2 (overlapped)");
     if (cfg->word_planes != 0 && cfg->word_planes != 2 && cfg->word_planes != 4)
         return fail(GOL_EINVAL, "word_planes must be 0 (auto), 2 or 4");
     if (cfg->word_planes == 4 && !gol::kDevKernels)
@@ -771,11 +776,15 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // build_plans) the band does run concurrently (trace_rank8_overlap_capped.csv),
     // but per-rank rates through the host-transport proxy stayed within -3..+3% of
     // blocking and bimodal at 2 ranks, and an RCCL exchange is itself a kernel that
-    // needs free slots: blocking stays the rank default.  GOL_DEV_OVERLAP = 1 / 0
-    // forces the overlap on / off (dev A/B and the tests of both paths).
+    // needs free slots: blocking stays the rank default.  gol_config.exchange_overlap
+    // chooses either mode (bench.py --gpus N times both); with it at 0 (auto),
+    // GOL_DEV_OVERLAP = 1 / 0 forces the overlap on / off (dev A/B).
     const int64_t Hx_ = (int64_t)g->Hx, R = (int64_t)g->R;
     bool want = group;
-    if (const char* ov = std::getenv("GOL_DEV_OVERLAP")) want = ov[0] == '1';
+    if (cfg->exchange_overlap)
+        want = cfg->exchange_overlap == 2;
+    else if (const char* ov = std::getenv("GOL_DEV_OVERLAP"))
+        want = ov[0] == '1';
     if ((int64_t)(h / (uint64_t)nranks) >= 2 * Hx_ && want) {
         SegDesc b = g->raw.back()[0];  // shrink Hx: out = own rows
         std::vector<SegDesc> band, inner;
@@ -1271,14 +1280,17 @@ gol_status exchange(gol_engine* e, hipStream_t st)
     const size_t S = e->stride;
     const bool has_up = e->rank > 0, has_dn = e->rank < e->nranks - 1;
     if (e->xfer == XFER_RCCL) {
+        // p2p operations to one peer inside a group are matched in issue order, so
+        // the self-loop communicator delivers the up rows to the up halo and the
+        // down rows to the down halo
         NCCL_TRY(ncclGroupStart());
         if (has_up) {
-            NCCL_TRY(ncclSend(b + e->Hx * S, n, ncclUint64, e->rank - 1, e->comm, st));
-            NCCL_TRY(ncclRecv(b, n, ncclUint64, e->rank - 1, e->comm, st));
+            NCCL_TRY(ncclSend(b + e->Hx * S, n, ncclUint64, e->peer_up, e->comm, st));
+            NCCL_TRY(ncclRecv(b, n, ncclUint64, e->peer_up, e->comm, st));
         }
         if (has_dn) {
-            NCCL_TRY(ncclSend(b + e->R * S, n, ncclUint64, e->rank + 1, e->comm, st));
-            NCCL_TRY(ncclRecv(b + (e->R + e->Hx) * S, n, ncclUint64, e->rank + 1, e->comm, st));
+            NCCL_TRY(ncclSend(b + e->R * S, n, ncclUint64, e->peer_dn, e->comm, st));
+            NCCL_TRY(ncclRecv(b + (e->R + e->Hx) * S, n, ncclUint64, e->peer_dn, e->comm, st));
         }
         NCCL_TRY(ncclGroupEnd());
         return GOL_OK;
@@ -1485,7 +1497,12 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     e->R = g.R;
     e->Hx = g.Hx;
     e->shared_device = shared_device;
-    st = init_common(e, h, w, cfg, &g);
+    // stripe engines run the streaming kernel even as the only rank, so that
+    // gol_round_schedule (host-only: no occupancy query for the resident plan)
+    // lists exactly the launches gol_step runs
+    gol_config c = *cfg;
+    c.resident = 1;
+    st = init_common(e, h, w, &c, &g);
     if (st != GOL_OK) {
         std::string msg = g_last_error;
         gol_destroy(e);
@@ -1516,7 +1533,26 @@ gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int ra
             gol_destroy(e);
             return fail(GOL_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(he));
         }
-        ncclResult_t r = ncclCommInitRank(&e->comm, nranks, u, rank);
+        // GOL_DEV_RCCL_SELF=1 (test hook, tests/test_gpu_rccl.py): RCCL refuses two
+        // ranks on one device, so a one-GPU box runs this rank's byte mover against
+        // a 1-rank communicator whose up and down peers are the rank itself -- each
+        // exchange sends the boundary rows to itself and its halos receive them
+        // (a caller's host transport that returns what it is sent does the same)
+        // (with an id of its own: every rank of the caller's job is rank 0 of its
+        // own communicator)
+        const char* selfv = std::getenv("GOL_DEV_RCCL_SELF");
+        const bool self_loop = selfv && selfv[0] == '1';
+        if (self_loop) {
+            ncclResult_t r = ncclGetUniqueId(&u);
+            if (r != ncclSuccess) {
+                gol_destroy(e);
+                return fail(GOL_ERCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+            }
+        }
+        e->peer_up = self_loop ? 0 : rank - 1;
+        e->peer_dn = self_loop ? 0 : rank + 1;
+        ncclResult_t r = self_loop ? ncclCommInitRank(&e->comm, 1, u, 0)
+                                   : ncclCommInitRank(&e->comm, nranks, u, rank);
         if (r != ncclSuccess) {
             gol_destroy(e);
             return fail(GOL_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));

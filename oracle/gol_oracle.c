@@ -325,6 +325,7 @@ static void bp_rows(const uint64_t* in, uint64_t* out, int64_t h, int64_t w, int
             uint64_t n3 = m & k1;
             uint64_t res = 0;
             for (int n = 0; n <= 8; n++) {
+                if (!(((birth | survive) >> n) & 1u)) continue; /* no cell takes this count */
                 uint64_t eq = ((n & 1) ? n0 : ~n0) & ((n & 2) ? n1 : ~n1) &
                               ((n & 4) ? n2 : ~n2) & ((n & 8) ? n3 : ~n3);
                 uint64_t sel = (((survive >> n) & 1u) ? alive : 0) |

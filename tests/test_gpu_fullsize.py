@@ -69,3 +69,37 @@ def test_c5_per_gpu_unit_vs_oracle(pkg, oracle, rule):
     got = digest_of(pkg, h, w, R, 16)
     g = oracle.bp_run(oracle.bp_random(h, w, 1), w, 16, R, threads=THREADS)
     assert got == oracle.bp_digest(g, w)
+
+
+def test_c3_conway_1000_generations_vs_depth1(pkg):
+    """The headline field under B3/S23 (still active after 1000 generations, unlike
+    B/S2's fixed point within ~10): the default engine's 1000 generations (62
+    full-depth age-skewed launches + a depth-8 one, graph replay) equal 1000
+    depth-1 launches of classic blocks."""
+    with pkg.Engine(N, N, rule=pkg.CONWAY, device=0) as e:
+        assert e.tb_depth == 16 and e.age_skew is not None
+        e.init_random(7)
+        e.step(999)
+        d999 = e.digest()
+        e.step(1)
+        d1000 = e.digest()
+    assert d999 != d1000, "field reached a fixed point: the check would be weak"
+    assert d1000 == digest_of(pkg, N, N, pkg.CONWAY, 1000, seed=7, streams=1, tb_depth=1,
+                              handoff=1)
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+def test_c5_full_field_one_gpu_vs_oracle(pkg, oracle, rule):
+    """The whole C5 field, 262144^2 (8 GiB per buffer), on ONE GPU with the default
+    engine (one stream of age-skewed launches; the 144 TCUPS configuration of
+    DESIGN.md §5) after one K = 16 launch, against the oracle's digest (24 GiB of
+    host memory)."""
+    n = 262144
+    R = oracle.REF_RULE if rule == "ref" else oracle.CONWAY
+    with pkg.Engine(n, n, rule=R, device=0) as e:
+        assert e.tb_depth == 16 and e.age_skew is not None, (e.tb_depth, e.age_skew)
+        e.init_random(1)
+        e.step(16)
+        got = e.digest()
+    g = oracle.bp_run(oracle.bp_random(n, n, 1), n, 16, R, threads=THREADS)
+    assert got == oracle.bp_digest(g, n)

@@ -1,19 +1,136 @@
-"""The RCCL halo path itself (gol_create_rank + ncclSend/Recv over xGMI), one
-process per GPU.  RCCL refuses two ranks on one device, so this needs a box with
-at least two GPUs and is skipped elsewhere (test_gpu_transport.py runs the same
-rank engines and schedule with a host transport on one GPU; bench.py --gpus N
-repeats this check as `rccl_selfcheck` before its timed run).
+"""The RCCL halo path itself (gol_create_rank + ncclSend/Recv), engine.cpp
+`exchange`, which replaces the reference's MPI_Sendrecv pair
+(Parallel_Life_MPI.cpp:113-116, :129-132, called at :218).
 
-Each rank advances its stripe of a B3/S23 field over several Hx-generation
-rounds; the stripe digests (order-independent sums) must add up to the digest of
-the whole field evolved by one engine, which the rest of the suite pins to the
-oracle.
+* On ONE GPU (every box): RCCL refuses two ranks on one device, so a rank engine
+  of an N-way split runs its byte mover against a 1-rank communicator whose up
+  and down peers are itself (GOL_DEV_RCCL_SELF=1: ncclCommInitRank with nranks 1,
+  then ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd on the engine's
+  stream every round).  Its halos then receive the stripe's own boundary rows.
+  That is checked three ways: against the oracle evolving the same "mirrored"
+  extended stripe round by round, against the same engine over a host transport
+  that returns what it is sent (bytewise, every chunk), and against a transport
+  that delivers dead rows (the exchange must change the result).
+* On boxes with >= 2 GPUs: one process per GPU, the stripe digests of a B3/S23
+  field must add up to the whole field evolved by one engine (bench.py --gpus N
+  repeats this as `rccl_selfcheck` before timing).
 """
+import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
+
+
+def mirrored_round(oracle, own, w, gens, rule, Hx, has_up, has_dn):
+    """One round of a self-looped rank: its halos hold its own first / last Hx
+    rows (where it has that neighbour), the extended stripe evolves `gens`
+    generations with dead cells beyond it, and its own rows are kept."""
+    parts = ([own[:Hx]] if has_up else []) + [own] + ([own[-Hx:]] if has_dn else [])
+    ext = np.concatenate(parts)
+    out = oracle.bp_run(ext, w, gens, rule)
+    top = Hx if has_up else 0
+    return out[top:top + own.shape[0]]
+
+
+def mirrored_steps(oracle, own, w, chunks, rule, Hx, has_up, has_dn):
+    """Every gol_step call starts a round; rounds are Hx generations, the last
+    one of a call what is left (engine.cpp step_schedule)."""
+    outs = []
+    for c in chunks:
+        left = c
+        while left:
+            g = min(left, Hx)
+            own = mirrored_round(oracle, own, w, g, rule, Hx, has_up, has_dn)
+            left -= g
+        outs.append(own)
+    return outs
+
+
+@pytest.mark.parametrize("overlap", [1, 2])
+@pytest.mark.parametrize("world,rank,K,Hx,rule", [
+    (2, 0, 8, 32, "conway"),     # bottom neighbour only
+    (2, 1, 16, 64, "conway"),    # top neighbour only
+    (3, 1, 8, 24, "highlife"),   # both
+    (4, 2, 16, 0, "ref"),        # both, default halo depth (8K)
+])
+def test_rccl_self_loop(pkg, oracle, monkeypatch, world, rank, K, Hx, rule, overlap):
+    """overlap 1: blocking exchanges on the compute stream; 2: the band launch,
+    then the exchange on the comm stream beside the interior launch."""
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    R = {"ref": oracle.REF_RULE, "conway": oracle.CONWAY, "highlife": oracle.HIGHLIFE}[rule]
+    h, w, seed = 1200, 2000, 21 + rank
+    g = oracle.bp_random(h, w, seed)
+    cfg = dict(rule=R, device=0, tb_depth=K, halo_depth=Hx, exchange_overlap=overlap)
+    with pkg.Engine(h, w, rank=rank, nranks=world, uid=pkg.unique_id(), **cfg) as e:
+        Hx_ = e.halo_depth
+        own = g[e.row0:e.row0 + e.rows]
+        chunks = [Hx_, 5, 2 * Hx_ + 3, 40]  # full rounds, partial ones, carried overlap
+        got = []
+        e.load_packed(own)
+        for c in chunks:
+            e.step(c)  # no sync: store/digest must order after the comm stream
+            got.append((e.store_packed(), e.digest()))
+    has_up, has_dn = rank > 0, rank < world - 1
+    want = mirrored_steps(oracle, own, w, chunks, R, Hx_, has_up, has_dn)
+    for i, (c, (a, dg), b) in enumerate(zip(chunks, got, want)):
+        assert (a == b).all(), f"chunk {i} ({c} generations)"
+        # the rank's live count covers its own rows
+        assert dg[0] == int(np.unpackbits(b.view(np.uint8)).sum())
+    # bytewise against the host transport that loops back what it is sent, and the
+    # exchange must matter: dead rows in the halos give a different field
+    loop = lambda su, sd: (su, sd)  # noqa: E731
+    dead = lambda su, sd: (None if su is None else bytes(len(su)),  # noqa: E731
+                           None if sd is None else bytes(len(sd)))
+    for tp, same in ((loop, True), (dead, False)):
+        with pkg.Engine(h, w, rank=rank, nranks=world, transport=tp, **cfg) as t:
+            t.load_packed(own)
+            res = []
+            for c in chunks:
+                t.step(c)
+                res.append((t.store_packed(), t.digest()))
+        if same:
+            for i, ((a, da), (b, db)) in enumerate(zip(got, res)):
+                assert (a == b).all() and da == db, f"RCCL vs host loopback, chunk {i}"
+        else:
+            assert any((a != b).any() for (a, _), (b, _) in zip(got, res)), \
+                "dead halos gave the same field: the exchange had no effect"
+
+
+def test_rccl_self_loop_c4_rank_shape(pkg, monkeypatch):
+    """The 8-way C4 per-rank shape (8192 own rows of 65536^2 + 2 x 128 halo rows,
+    default K = 16, age-skewed one-round launches, default block kind): 1 MiB
+    messages through RCCL every round, bytewise equal to the host loopback."""
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    n, world, rank, gens = 65536, 8, 3, 2 * 128 + 40
+    out = []
+    for mode in ("rccl", "host"):
+        kw = dict(uid=pkg.unique_id()) if mode == "rccl" else dict(transport=lambda su, sd: (su, sd))
+        with pkg.Engine(n, n, rule=pkg.CONWAY, device=0, rank=rank, nranks=world, **kw) as e:
+            assert e.halo_depth == 128
+            e.init_random(3)
+            e.step(gens)
+            out.append((e.digest(), e.store_packed()))
+    assert out[0][0] == out[1][0]
+    assert (out[0][1] == out[1][1]).all()
+
+
+def test_rccl_self_loop_two_communicators(pkg, monkeypatch):
+    """A second engine on another self-loop communicator in the same process, and
+    destroy/re-create: communicators are per engine."""
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    for _ in range(2):
+        a = pkg.Engine(512, 640, rule=pkg.CONWAY, device=0, rank=1, nranks=3, uid=pkg.unique_id())
+        b = pkg.Engine(512, 640, rule=pkg.CONWAY, device=0, rank=1, nranks=3, uid=pkg.unique_id())
+        a.init_random(1)
+        b.init_random(1)
+        a.step(100)
+        a.sync()
+        b.step(100)
+        assert a.digest() == b.digest()
+        a.close()
+        b.close()
 
 
 def worker(rank, n, uid, h, w, gens, q):
