@@ -23,8 +23,10 @@ prints one JSON line.
     wave-instruction x slots per lane group and generation (24 for B/S2: 16
     v_bitop3 + 2 DPP moves and 2 v_alignbit at two slots each; static count of
     the steady-state loop, profiles/r02/valu_mix.json) / the mean HIP-event
-    launch time x concurrent streams; peak = 1024 SIMDs x the best measured
-    full-rate VALU issue rate (profiles/r01/valu_rate.json); frac <= 1;
+    launch time x concurrent streams; peak = the spec issue rate, 1024 SIMD-32 x
+    2.4 GHz / 2 cycles per wave64 instruction = 1228.8 G/s (MI355X_MICROARCH.md),
+    with the best measured rate beside it (profiles/r01/valu_rate.json, 1067 G/s:
+    peak_measured, frac_vs_measured);
   * valu.issue_frac: ALL VALU instructions per launch (rocprofv3 SQ_INSTS_VALU
     of this configuration, committed in profiles/r02/counters.json: warm-up,
     masks and halo work included) at the same peak;
@@ -51,6 +53,9 @@ METRIC = "cell updates/sec (GCUPS) at 65536^2, 1/2/4/8 GPUs; % of HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_CELL_GEN = 0.25
 SIMDS = 1024  # 256 CUs x 4
+# MI355X_MICROARCH.md: each SIMD-32 issues one wave64 VALU instruction per 2 cycles
+# at the 2.4 GHz engine clock -> 1.2 G wave-instruction slots per SIMD per second
+SPEC_SLOT_RATE = 2.4e9 / 2
 CELLS_PER_WAVE_INSTR = 64 * 64  # 64 lanes x one 64-column lane group (2 planes)
 # VALU issue slots per lane group and generation of the stage logic (v_bitop3 = 1,
 # DPP move and v_alignbit = 2 each): tools/valu_mix.py, profiles/r02/valu_mix.json
@@ -357,7 +362,8 @@ def main():
     # concurrently, each timed on its own stream: per-launch rate x streams
     streams = max(1, tm.get("streams", 1))
     launch_s = avg_launch_ms / 1e3
-    peak_slot_rate = SIMDS * valu_peak_rate()  # wave-instruction slots / s
+    peak_slot_rate = SIMDS * SPEC_SLOT_RATE  # wave-instruction slots / s (spec)
+    meas_slot_rate = SIMDS * valu_peak_rate()  # best measured issue rate
     slots_per_launch = cg_per_launch / CELLS_PER_WAVE_INSTR * STAGE_SLOTS[a.rule]
     valu_achieved = slots_per_launch * streams / launch_s
     cfg_key = {"size": n, "rule": a.rule, "tb_depth": eng.tb_depth, "streams": streams,
@@ -399,6 +405,12 @@ def main():
                 "unit": "G VALU issue slots/s (stage logic: v_bitop3 1 slot, DPP move and "
                         "v_alignbit 2 slots)",
                 "frac": round(valu_achieved / peak_slot_rate, 4),
+                "peak_from": "MI355X_MICROARCH.md: 1024 SIMD-32 x 2.4 GHz / 2 cycles per wave64 "
+                             "VALU instruction",
+                "peak_measured": round(meas_slot_rate / 1e9, 1),
+                "frac_vs_measured": round(valu_achieved / meas_slot_rate, 4),
+                "peak_measured_from": "profiles/r01/valu_rate.json (v_bitop3, 2 waves/SIMD, best "
+                                      "code placement) x 1024 SIMDs",
                 "traffic": traffic,
                 "kernel": "life_res_kernel" if eng.resident else "life_tb_kernel",
                 "avg_launch_ms": round(avg_launch_ms, 4),
@@ -411,8 +423,8 @@ def main():
                     "insts_per_launch": insts,
                     "issue_frac": (round(insts * streams / launch_s / peak_slot_rate, 4)
                                    if insts else None),
-                    "peak_from": "profiles/r01/valu_rate.json (v_bitop3, 2 waves/SIMD, best "
-                                 "code placement) x 1024 SIMDs",
+                    "issue_frac_vs_measured": (round(insts * streams / launch_s / meas_slot_rate, 4)
+                                               if insts else None),
                     "counters_from": (f"profiles/r02/counters.json (record of rows_per_wave "
                                       f"{ctr.get('rows_per_wave')})" if insts else None),
                 },

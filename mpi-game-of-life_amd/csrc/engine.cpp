@@ -193,6 +193,9 @@ struct gol_engine {
     // other engines launch on this device concurrently (composite parts, group
     // members sharing a GPU): the age skew's dispatch-order premise does not hold
     bool shared_device = false;
+    // registered in the device's waiting-kernel registry (wait_registry) as the
+    // hand-off engine / as a resident engine
+    bool reg_hand = false, reg_res = false;
     hipEvent_t ev_ready = nullptr, ev_copied = nullptr;
 
     // exchange/compute overlap (multi-rank): the last launch of a full round is
@@ -366,6 +369,10 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
                 }
                 if (hand && blocks_max < 2) continue;  // nothing to hand over
                 const int64_t n = (units + simds - 1) / simds;
+                // hand-off blocks wait for other wavefronts of their launch: only
+                // launches of one round (every wavefront resident at once, so a
+                // producer never queues behind the consumers waiting for it)
+                if (hand && n > occ) continue;
                 const int64_t full = n / occ, rem = n % occ;
                 const double slots =
                     (double)full * std::max(2, occ) + (rem ? (double)std::max<int64_t>(2, rem) : 0.0);
@@ -865,6 +872,42 @@ void step_schedule(uint32_t K, uint64_t Hx, bool overlap, bool halo_fresh, uint6
 
 gol_status plan_resident(gol_engine* e, const gol_config* cfg);
 
+// Kernels that wait for other wavefronts of their own launch -- hand-off row blocks
+// (life_stencil.h) and the resident kernel -- need every wavefront they wait for
+// to get a slot.  Their plans guarantee it for the launch alone on the device:
+// hand-off launches are one round of the occupancy query (pick_rows_per_wave), the
+// resident grid is at most one workgroup per CU (plan_resident).  Launches of
+// other engines of this process would share the slots, so the process keeps, per
+// device: at most one engine with hand-off blocks, and none while a resident engine
+// lives (resident launches of several engines are ordered on one stream,
+// resident_stream; classic blocks and composite parts never wait, so they may run
+// beside either).  An engine that cannot get the kind it would plan runs classic
+// blocks / the streaming kernel instead (gol_plan_handoff, gol_plan_resident
+// report it).  GOL_DEV_SHARED_WAITS=1 turns the registry off (dev sweeps that
+// step their engines one at a time).
+struct WaitReg {
+    gol_engine* hand = nullptr;
+    int resident = 0;
+};
+std::mutex g_wait_mu;
+std::map<int, WaitReg> g_wait_reg;
+
+bool wait_registry_off()
+{
+    const char* v = std::getenv("GOL_DEV_SHARED_WAITS");
+    return v && v[0] == '1';
+}
+
+void wait_release(gol_engine* e)
+{
+    if (!e->reg_hand && !e->reg_res) return;
+    std::lock_guard<std::mutex> lock(g_wait_mu);
+    WaitReg& r = g_wait_reg[e->device];
+    if (e->reg_hand && r.hand == e) r.hand = nullptr;
+    if (e->reg_res) r.resident--;
+    e->reg_hand = e->reg_res = false;
+}
+
 // Common construction; geometry (row0, R, Hx, rank) already set.
 gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* cfg,
                        const RankGeom* geom)
@@ -969,9 +1012,33 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
     }
     HIP_TRY(hipMalloc(&e->d_acc, 2 * sizeof(unsigned long long)));
     HIP_TRY(hipMalloc(&e->d_flag, sizeof(int)));
-    gol_status st = build_plans(e, raw);
-    if (st != GOL_OK) return st;
-    st = plan_resident(e, cfg);
+    gol_status st = GOL_OK;
+    {
+        // plan and register under the lock, so that engines created by several
+        // threads see each other (wait_release)
+        std::lock_guard<std::mutex> lock(g_wait_mu);
+        const bool off = wait_registry_off();
+        const WaitReg reg = g_wait_reg[e->device];
+        gol_config c = *cfg;
+        if (!off && (reg.hand || reg.resident)) e->handoff = 1;
+        if (!off && reg.hand) c.resident = 1;
+        st = build_plans(e, raw);
+        if (st == GOL_OK) st = plan_resident(e, &c);
+        if (st == GOL_OK && !off) {
+            WaitReg& r = g_wait_reg[e->device];
+            if (e->res.on) {
+                e->reg_res = true;
+                r.resident++;
+            } else {
+                bool hand = false;
+                for (const auto& pl : e->plans) hand |= pl.hand && pl.multi_blk;
+                if (hand && e->side[0]) {
+                    e->reg_hand = true;
+                    r.hand = e;
+                }
+            }
+        }
+    }
     if (st != GOL_OK) return st;
     HIP_TRY(hipStreamSynchronize(e->stream));
     return GOL_OK;
@@ -1058,7 +1125,12 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
         // the generic-mask rule keeps 8 rows per wavefront only with spills
         if (e->rule == gol::RULE_GENERIC && M > 6 && cfg->rows_per_wave != (uint32_t)M) continue;
         const int64_t NR = (int64_t)gol::kResWaves * M;
-        const int64_t max_bands = std::min<int64_t>(cus / strips, h);
+        // tiles per CU: the kernel's occupancy, capped by GOL_DEV_RES_PER_CU (dev
+        // A/B; default 1)
+        int per_cu = 1;
+        if (const char* v = std::getenv("GOL_DEV_RES_PER_CU")) per_cu = std::max(1, std::atoi(v));
+        per_cu = std::min(per_cu, gol::resident_blocks_per_cu(M, e->rule));
+        const int64_t max_bands = std::min<int64_t>((int64_t)cus * per_cu / strips, h);
         for (int64_t nb = 1; nb <= max_bands; ++nb) {
             const int64_t B = (h + nb - 1) / nb;
             const int64_t bands = (h + B - 1) / B;
@@ -1142,6 +1214,9 @@ gol_status step_resident(gol_engine* e, uint64_t generations)
         a.flag_base = r.flag_base;
         a.birth = e->birth;
         a.survive = e->survive;
+#if GOL_EXP
+        a.wlog = g_dev_wave_log;
+#endif
         hipEvent_t e0, e1;
         GOL_TRY(timing_begin(e, rs, &e0, &e1));
         HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, rs));
@@ -1663,6 +1738,7 @@ void gol_destroy(gol_engine* e)
         if (n->comm_stream) (void)hipStreamSynchronize(n->comm_stream);
         if (n->band_stream) (void)hipStreamSynchronize(n->band_stream);
     }
+    wait_release(e);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->host_xfer) (void)hipHostFree(e->host_xfer);
     if (e->up) e->up->down = nullptr;

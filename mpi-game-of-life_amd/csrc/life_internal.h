@@ -161,6 +161,7 @@ struct ResArgs {
     int32_t gens;         // generations of this launch
     uint32_t flag_base;
     uint32_t birth, survive;
+    uint64_t* wlog;       // dev timing builds only (GOL_EXP & 2048): 4 words per wavefront
 };
 hipError_t launch_resident(const ResArgs& a, int rows, RuleKind rule, int grid, hipStream_t s);
 int resident_blocks_per_cu(int rows, RuleKind rule);

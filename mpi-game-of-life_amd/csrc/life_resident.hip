@@ -44,8 +44,11 @@ namespace gol {
 
 namespace {
 
-constexpr int kResLdsWords = 96 * 1024 / 8;  // > 80 KB: one workgroup per CU
-static_assert(2 * 2 * kResWaves * 64 * 2 <= kResLdsWords, "edge H3 rows fit the LDS block");
+// LDS of a workgroup: the edge H3 rows (2 slots x top/bottom x waves x 16 B per
+// lane), a zero row and the per-wave progress words -- 66 KB, so that two
+// workgroups fit a CU (the occupancy query decides how many tiles the grid may have)
+constexpr int kResEdgeWords = 2 * 2 * kResWaves * 64 * 2;
+constexpr int kResLdsWords = kResEdgeWords + 128 + kResWaves / 2;
 
 // H3 of a row: bit-sliced sum (s) and carry (c) of each cell and its 2
 // horizontal neighbours (life_stencil.h stage_step's first half).
@@ -149,13 +152,17 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     bool gave_up = false;
     // edge H3 rows through LDS: slot p = [top/bottom][wave][lane], 2 slots
     auto put_edges = [&](int p) {
-        if constexpr (!(GOL_EXP & 32)) {
-            uint4* ed = ed4 + p * (2 * W * 64);
-            ed[wv * 64 + lane] = uint4{s[0].v[0], s[0].v[1], c[0].v[0], c[0].v[1]};
-            ed[(W + wv) * 64 + lane] = uint4{s[M - 1].v[0], s[M - 1].v[1], c[M - 1].v[0],
-                                             c[M - 1].v[1]};
-        }
+        uint4* ed = ed4 + p * (2 * W * 64);
+        ed[wv * 64 + lane] = uint4{s[0].v[0], s[0].v[1], c[0].v[0], c[0].v[1]};
+        ed[(W + wv) * 64 + lane] = uint4{s[M - 1].v[0], s[M - 1].v[1], c[M - 1].v[0],
+                                         c[M - 1].v[1]};
     };
+    // after the edge slots: a zero row (the edges of the missing neighbours of the
+    // first and last wave), then the per-wave progress words: the edges of
+    // generation n of the launch are in their slot once cnt[wave] >= n
+    uint4* const zero4 = ed4 + 4 * W * 64;
+    uint32_t* const cnt = reinterpret_cast<uint32_t*>(zero4 + 64);
+    if (wv == 0) zero4[lane] = uint4{0u, 0u, 0u, 0u};
     auto rule_row = [&](int i, const Pl<2>& as, const Pl<2>& ac, const Pl<2>& es,
                         const Pl<2>& ec) {
 #pragma unroll
@@ -166,37 +173,90 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
             x[i].v[q] = y;
         }
     };
+    // After generation g+1 of an epoch only rows [b0 - K + g + 1, b1 + K - g - 1)
+    // of the held range are exact: this wave computes generation g+1 iff g < gmax
+    // (the rows its neighbours would compute from it otherwise are discarded), and
+    // once off it stays off for the rest of the epoch.
+    const int32_t gmax = (int32_t)min<int64_t>(r0 + M - (b0 - a.K) - 1, b1 + a.K - 1 - r0);
+    const bool has_up = wv > 0, has_dn = wv < W - 1;
+    // the first / last wave waits on its own word (always current) instead
+    uint32_t* const cnt_up = cnt + (has_up ? wv - 1 : wv);
+    uint32_t* const cnt_dn = cnt + (has_dn ? wv + 1 : wv);
+    auto word = [](uint32_t* p) {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+#if GOL_EXP & 2048
+    // dev timing build: per-wave cycles waiting for neighbour waves, in epoch
+    // hand-offs, and in all (s_memtime), logged at the end
+    uint64_t t_wait = 0, t_epoch = 0, t_beg = __builtin_amdgcn_s_memtime(), t_ep0 = 0;
+#endif
     for (int32_t done = 0; done < a.gens;) {
         const int32_t k = min(a.K, a.gens - done);
 #pragma unroll
         for (int i = 0; i < M; ++i) h3_row(x[i], s[i], c[i]);
         put_edges(0);
+        // (a wave whose rows are never exact this epoch releases its neighbours now)
+        if (lane == 0)
+            __hip_atomic_store(cnt + wv, (uint32_t)(gmax > 0 ? done : done + k), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        // Generations: no workgroup barrier.  Each wave waits only for its two
+        // neighbour waves' edges of the generation it starts from (their progress
+        // words in LDS), so the waves of a SIMD drift apart and one's VALU work
+        // covers another's LDS round trip.  LDS executes a wave's accesses in
+        // order: the edges are stored before the progress word, and read after it.
+        // A slot is rewritten two generations later, after both neighbours have
+        // published the generation in between (which they do after reading it).
         for (int32_t g = 0; g < k; ++g) {
-            // after generation g+1 of the epoch only rows [lo, hi) of the held range
-            // are exact: a wave with none of them skips the work (the rows its
-            // neighbours would compute from it are discarded), and the H3 of the
-            // next generation is needed exactly for the rows this one computes
-            const int64_t lo = b0 - a.K + g + 1, hi = b1 + a.K - g - 1;
-            const bool on = r0 + M > lo && r0 < hi;
-            if constexpr (!(GOL_EXP & 16)) __syncthreads();
-            Pl<2> us = zero_pl(), uc = zero_pl(), ds = zero_pl(), dc = zero_pl();
-            if constexpr (!(GOL_EXP & 32)) {
+            if (g < gmax) {
+                const uint32_t need = (uint32_t)(done + g);
                 const uint4* ed = ed4 + (g & 1) * (2 * W * 64);
-                if (wv > 0) {
-                    const uint4 t = ed[(W + wv - 1) * 64 + lane];
-                    us.v[0] = t.x; us.v[1] = t.y; uc.v[0] = t.z; uc.v[1] = t.w;
-                }
-                if (wv < W - 1) {
-                    const uint4 t = ed[(wv + 1) * 64 + lane];
-                    ds.v[0] = t.x; ds.v[1] = t.y; dc.v[0] = t.z; dc.v[1] = t.w;
-                }
-            }
-            if (on) {
-                // interior rows first (no LDS operand: they cover the LDS read),
-                // then the edge rows; next generation's H3: edges first, so their
-                // LDS write is covered by the interior H3 and the barrier
+                const uint4* pu = has_up ? ed + (W + wv - 1) * 64 + lane : zero4 + lane;
+                const uint4* pd = has_dn ? ed + (wv + 1) * 64 + lane : zero4 + lane;
+#if GOL_EXP & 2048
+                const uint64_t tw0 = __builtin_amdgcn_s_memtime();
+#endif
+                uint32_t cu = word(cnt_up), cd = word(cnt_dn);
+                asm volatile("" ::: "memory");  // edge reads issue after the progress reads
+                uint4 tu = *pu, td = *pd;
+                // interior rows first: no LDS operand, they cover the round trip
 #pragma unroll
-                for (int i = 1; i < M - 1; ++i) rule_row(i, s[i - 1], c[i - 1], s[i + 1], c[i + 1]);
+                for (int i = 1; i < M - 1; ++i) {
+                    rule_row(i, s[i - 1], c[i - 1], s[i + 1], c[i + 1]);
+                    asm volatile("" : "+v"(x[i].v[0]), "+v"(x[i].v[1]));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (__builtin_amdgcn_readfirstlane(min((int32_t)(cu - need), (int32_t)(cd - need))) < 0) {
+                    // a neighbour is behind: poll the words alone, then re-read
+                    for (int n = 0;; ++n) {
+                        if (n > kPollLimit) {  // lost: flag it, go on so the launch drains
+                            __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(0);
+                        asm volatile("" ::: "memory");
+                        cu = word(cnt_up);
+                        cd = word(cnt_dn);
+                        if (__builtin_amdgcn_readfirstlane(
+                                min((int32_t)(cu - need), (int32_t)(cd - need))) >= 0)
+                            break;
+                    }
+                    asm volatile("" ::: "memory");
+                    tu = *pu;
+                    td = *pd;
+                }
+#if GOL_EXP & 2048
+                {
+                    // wait for the edge values themselves before the stamp
+                    uint32_t v = tu.x ^ td.x;
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
+                    t_wait += __builtin_amdgcn_s_memtime() - tw0;
+                    if (v == 0x5a5a5a5au) tu.y ^= 1u;  // keeps v live (never taken on real data)
+                }
+#endif
+                Pl<2> us, uc, ds, dc;
+                us.v[0] = tu.x; us.v[1] = tu.y; uc.v[0] = tu.z; uc.v[1] = tu.w;
+                ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
                 if constexpr (M == 1) {
                     rule_row(0, us, uc, ds, dc);
                 } else {
@@ -204,14 +264,26 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
                     rule_row(M - 1, s[M - 2], c[M - 2], ds, dc);
                 }
                 if (g + 1 < k) {
+                    // next generation's H3: the edge rows first, published at once
                     h3_row(x[0], s[0], c[0]);
                     if constexpr (M > 1) h3_row(x[M - 1], s[M - 1], c[M - 1]);
                     put_edges((g + 1) & 1);
+                    asm volatile("" ::: "memory");  // progress word after the edges
+                    if (lane == 0)
+                        __hip_atomic_store(cnt + wv, need + 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
                     for (int i = 1; i < M - 1; ++i) h3_row(x[i], s[i], c[i]);
                 }
+            } else if (g == gmax && lane == 0) {
+                // off from here on: release the neighbours for the rest of the epoch
+                __hip_atomic_store(cnt + wv, (uint32_t)(done + k), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
+#if GOL_EXP & 2048
+        t_ep0 = __builtin_amdgcn_s_memtime();
+#endif
         done += k;
         ++epoch;
         // publish the band rows into the buffer of this epoch's result
@@ -251,7 +323,24 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
             const bool own = r >= b0 && r < b1;
             if (!own || halo_lane) x[i] = fetch(nb, r);
         }
+#if GOL_EXP & 2048
+        {
+            uint32_t v = x[0].v[0];
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(v));
+            x[0].v[0] = v;
+            t_epoch += __builtin_amdgcn_s_memtime() - t_ep0;
+        }
+#endif
     }
+#if GOL_EXP & 2048
+    if (a.wlog && lane == 0) {
+        uint64_t* wl = a.wlog + ((int64_t)blockIdx.x * W + wv) * 4;
+        wl[0] = __builtin_amdgcn_s_memtime() - t_beg;
+        wl[1] = t_wait;
+        wl[2] = t_epoch;
+        wl[3] = (uint64_t)tile << 32 | (uint32_t)gmax;
+    }
+#endif
 }
 
 template <int M>

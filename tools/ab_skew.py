@@ -17,6 +17,9 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import __graft_entry__ as entry  # noqa: E402
 
+# engines of this tool are stepped one at a time: no waiting-kernel registry
+os.environ.setdefault("GOL_DEV_SHARED_WAITS", "1")
+
 
 def main():
     p = argparse.ArgumentParser()

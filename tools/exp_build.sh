@@ -1,7 +1,7 @@
 #!/bin/bash
 # Dev: build timing-experiment variants of libgol.so (GOL_EXP bits, see
-# life_stencil.h: 1-8; life_resident.hip: 16 no barrier, 32 no LDS exchange, 64 no
-# neighbour waits) as mpi-game-of-life_amd/libgol_exp<N>.so.  Results of these
+# life_stencil.h: 1-8; life_resident.hip: 64 no epoch waits between tiles,
+# 2048 per-wave cycle stamps of the resident kernel) as mpi-game-of-life_amd/libgol_exp<N>.so.  Results of these
 # libraries are not valid fields; they exist to time pieces of the hand-off.
 # Usage: tools/exp_build.sh N [N ...]
 set -e

@@ -15,6 +15,9 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import __graft_entry__ as entry  # noqa: E402
 
+# engines of this tool are stepped one at a time: no waiting-kernel registry
+os.environ.setdefault("GOL_DEV_SHARED_WAITS", "1")
+
 p = argparse.ArgumentParser()
 p.add_argument("--size", type=int, default=65536)
 p.add_argument("--width", type=int, default=0)

@@ -24,6 +24,9 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import __graft_entry__ as entry  # noqa: E402
 
+# engines of this tool are stepped one at a time: no waiting-kernel registry
+os.environ.setdefault("GOL_DEV_SHARED_WAITS", "1")
+
 
 NOOP_C = """#include <stdint.h>
 int gol_noop_exchange(void* ctx, const void* su, void* ru, const void* sd, void* rd, uint64_t n)
