@@ -1125,12 +1125,7 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
         // the generic-mask rule keeps 8 rows per wavefront only with spills
         if (e->rule == gol::RULE_GENERIC && M > 6 && cfg->rows_per_wave != (uint32_t)M) continue;
         const int64_t NR = (int64_t)gol::kResWaves * M;
-        // tiles per CU: the kernel's occupancy, capped by GOL_DEV_RES_PER_CU (dev
-        // A/B; default 1)
-        int per_cu = 1;
-        if (const char* v = std::getenv("GOL_DEV_RES_PER_CU")) per_cu = std::max(1, std::atoi(v));
-        per_cu = std::min(per_cu, gol::resident_blocks_per_cu(M, e->rule));
-        const int64_t max_bands = std::min<int64_t>((int64_t)cus * per_cu / strips, h);
+        const int64_t max_bands = std::min<int64_t>(cus / strips, h);
         for (int64_t nb = 1; nb <= max_bands; ++nb) {
             const int64_t B = (h + nb - 1) / nb;
             const int64_t bands = (h + B - 1) / B;

@@ -45,10 +45,15 @@ namespace gol {
 namespace {
 
 // LDS of a workgroup: the edge H3 rows (2 slots x top/bottom x waves x 16 B per
-// lane), a zero row and the per-wave progress words -- 66 KB, so that two
-// workgroups fit a CU (the occupancy query decides how many tiles the grid may have)
+// lane), a zero row and the per-wave progress words, in a 96 KB block (> 80 KB:
+// one workgroup per CU).  Two tiles per CU (8 rows each at 4096^2, 66 KB each, SGPRs
+// capped at 80 so that the hardware admits 8 waves per SIMD) ran 17.9 against 22.7
+// TCUPS: the halo work grows by half and the extra waves do not hide it
+// (profiles/r03/c2_tiles_per_cu.txt).
 constexpr int kResEdgeWords = 2 * 2 * kResWaves * 64 * 2;
-constexpr int kResLdsWords = kResEdgeWords + 128 + kResWaves / 2;
+constexpr int kResLdsWords = 96 * 1024 / 8;
+static_assert(kResEdgeWords + 128 + kResWaves <= kResLdsWords,
+              "edge H3 rows, the zero row and the progress words fit the LDS block");
 
 // H3 of a row: bit-sliced sum (s) and carry (c) of each cell and its 2
 // horizontal neighbours (life_stencil.h stage_step's first half).
@@ -151,17 +156,20 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     uint32_t epoch = 0;
     bool gave_up = false;
     // edge H3 rows through LDS: slot p = [top/bottom][wave][lane], 2 slots
-    auto put_edges = [&](int p) {
-        uint4* ed = ed4 + p * (2 * W * 64);
-        ed[wv * 64 + lane] = uint4{s[0].v[0], s[0].v[1], c[0].v[0], c[0].v[1]};
-        ed[(W + wv) * 64 + lane] = uint4{s[M - 1].v[0], s[M - 1].v[1], c[M - 1].v[0],
-                                         c[M - 1].v[1]};
+    auto put_top = [&](int p) {
+        ed4[p * (2 * W * 64) + wv * 64 + lane] = uint4{s[0].v[0], s[0].v[1], c[0].v[0], c[0].v[1]};
+    };
+    auto put_bot = [&](int p) {
+        ed4[p * (2 * W * 64) + (W + wv) * 64 + lane] =
+            uint4{s[M - 1].v[0], s[M - 1].v[1], c[M - 1].v[0], c[M - 1].v[1]};
     };
     // after the edge slots: a zero row (the edges of the missing neighbours of the
-    // first and last wave), then the per-wave progress words: the edges of
-    // generation n of the launch are in their slot once cnt[wave] >= n
+    // first and last wave), then two progress words per wave: the top / bottom
+    // edge of generation n of the launch is in its slot once top[wave] / bot[wave]
+    // >= n
     uint4* const zero4 = ed4 + 4 * W * 64;
-    uint32_t* const cnt = reinterpret_cast<uint32_t*>(zero4 + 64);
+    uint32_t* const prog_top = reinterpret_cast<uint32_t*>(zero4 + 64);
+    uint32_t* const prog_bot = prog_top + W;
     if (wv == 0) zero4[lane] = uint4{0u, 0u, 0u, 0u};
     auto rule_row = [&](int i, const Pl<2>& as, const Pl<2>& ac, const Pl<2>& es,
                         const Pl<2>& ec) {
@@ -180,10 +188,28 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     const int32_t gmax = (int32_t)min<int64_t>(r0 + M - (b0 - a.K) - 1, b1 + a.K - 1 - r0);
     const bool has_up = wv > 0, has_dn = wv < W - 1;
     // the first / last wave waits on its own word (always current) instead
-    uint32_t* const cnt_up = cnt + (has_up ? wv - 1 : wv);
-    uint32_t* const cnt_dn = cnt + (has_dn ? wv + 1 : wv);
+    uint32_t* const wait_up = has_up ? prog_bot + wv - 1 : prog_top + wv;
+    uint32_t* const wait_dn = has_dn ? prog_top + wv + 1 : prog_bot + wv;
     auto word = [](uint32_t* p) {
         return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto set_word = [&](uint32_t* p, uint32_t v) {
+        if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    // spin until *p >= need (after a first read that came back short), then re-read
+    // the edge: progress read before edge read, LDS in order per wave
+    auto await = [&](uint32_t* p, uint32_t need, const uint4* pe, uint4& t) {
+        for (int n = 0;; ++n) {
+            if (n > kPollLimit) {  // lost: flag it, go on so the launch drains
+                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(0);
+            asm volatile("" ::: "memory");
+            if (__builtin_amdgcn_readfirstlane((int32_t)(word(p) - need)) >= 0) break;
+        }
+        asm volatile("" ::: "memory");
+        t = *pe;
     };
 #if GOL_EXP & 2048
     // dev timing build: per-wave cycles waiting for neighbour waves, in epoch
@@ -194,29 +220,33 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
         const int32_t k = min(a.K, a.gens - done);
 #pragma unroll
         for (int i = 0; i < M; ++i) h3_row(x[i], s[i], c[i]);
-        put_edges(0);
+        put_top(0);
+        put_bot(0);
         // (a wave whose rows are never exact this epoch releases its neighbours now)
-        if (lane == 0)
-            __hip_atomic_store(cnt + wv, (uint32_t)(gmax > 0 ? done : done + k), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        set_word(prog_top + wv, (uint32_t)(gmax > 0 ? done : done + k));
+        set_word(prog_bot + wv, (uint32_t)(gmax > 0 ? done : done + k));
         __syncthreads();
-        // Generations: no workgroup barrier.  Each wave waits only for its two
-        // neighbour waves' edges of the generation it starts from (their progress
-        // words in LDS), so the waves of a SIMD drift apart and one's VALU work
-        // covers another's LDS round trip.  LDS executes a wave's accesses in
-        // order: the edges are stored before the progress word, and read after it.
-        // A slot is rewritten two generations later, after both neighbours have
-        // published the generation in between (which they do after reading it).
+        // Generations: no workgroup barrier.  A wave's first row needs the upper
+        // neighbour wave's bottom edge, its last row the lower neighbour's top edge;
+        // each edge has its own progress word in LDS, and each of the wave's edge
+        // rows is computed, its H3 published and its word raised as soon as the one
+        // edge it needs is in, at raised priority (the neighbour waits for it); the
+        // interior rows fill the LDS round trips.  So the chain across a wave seam
+        // is one edge row per generation, and the waves of a SIMD drift apart.  LDS
+        // executes a wave's accesses in order: edges are stored before their word
+        // and read after it.  An edge slot is rewritten two generations later, after
+        // the wave that reads it has raised the word it publishes after that read
+        // (which this wave waits for before computing the row).
         for (int32_t g = 0; g < k; ++g) {
             if (g < gmax) {
                 const uint32_t need = (uint32_t)(done + g);
-                const uint4* ed = ed4 + (g & 1) * (2 * W * 64);
-                const uint4* pu = has_up ? ed + (W + wv - 1) * 64 + lane : zero4 + lane;
-                const uint4* pd = has_dn ? ed + (wv + 1) * 64 + lane : zero4 + lane;
+                const int p = g & 1, q = (g + 1) & 1;
+                const uint4* pu = has_up ? ed4 + p * (2 * W * 64) + (W + wv - 1) * 64 + lane : zero4 + lane;
+                const uint4* pd = has_dn ? ed4 + p * (2 * W * 64) + (wv + 1) * 64 + lane : zero4 + lane;
 #if GOL_EXP & 2048
                 const uint64_t tw0 = __builtin_amdgcn_s_memtime();
 #endif
-                uint32_t cu = word(cnt_up), cd = word(cnt_dn);
+                const uint32_t wu = word(wait_up), wd = word(wait_dn);
                 asm volatile("" ::: "memory");  // edge reads issue after the progress reads
                 uint4 tu = *pu, td = *pd;
                 // interior rows first: no LDS operand, they cover the round trip
@@ -226,59 +256,62 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
                     asm volatile("" : "+v"(x[i].v[0]), "+v"(x[i].v[1]));
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if (__builtin_amdgcn_readfirstlane(min((int32_t)(cu - need), (int32_t)(cd - need))) < 0) {
-                    // a neighbour is behind: poll the words alone, then re-read
-                    for (int n = 0;; ++n) {
-                        if (n > kPollLimit) {  // lost: flag it, go on so the launch drains
-                            __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(0);
-                        asm volatile("" ::: "memory");
-                        cu = word(cnt_up);
-                        cd = word(cnt_dn);
-                        if (__builtin_amdgcn_readfirstlane(
-                                min((int32_t)(cu - need), (int32_t)(cd - need))) >= 0)
-                            break;
-                    }
-                    asm volatile("" ::: "memory");
-                    tu = *pu;
-                    td = *pd;
-                }
+                if (__builtin_amdgcn_readfirstlane((int32_t)(wu - need)) < 0) await(wait_up, need, pu, tu);
 #if GOL_EXP & 2048
                 {
-                    // wait for the edge values themselves before the stamp
-                    uint32_t v = tu.x ^ td.x;
+                    uint32_t v = tu.x;
                     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
                     t_wait += __builtin_amdgcn_s_memtime() - tw0;
                     if (v == 0x5a5a5a5au) tu.y ^= 1u;  // keeps v live (never taken on real data)
                 }
 #endif
-                Pl<2> us, uc, ds, dc;
+                __builtin_amdgcn_s_setprio(2);
+                Pl<2> us, uc;
                 us.v[0] = tu.x; us.v[1] = tu.y; uc.v[0] = tu.z; uc.v[1] = tu.w;
-                ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
                 if constexpr (M == 1) {
+                    if (__builtin_amdgcn_readfirstlane((int32_t)(wd - need)) < 0) await(wait_dn, need, pd, td);
+                    Pl<2> ds, dc;
+                    ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
                     rule_row(0, us, uc, ds, dc);
+                    if (g + 1 < k) {
+                        h3_row(x[0], s[0], c[0]);
+                        put_top(q);
+                        put_bot(q);
+                        asm volatile("" ::: "memory");  // progress words after the edges
+                        set_word(prog_top + wv, need + 1u);
+                        set_word(prog_bot + wv, need + 1u);
+                    }
                 } else {
                     rule_row(0, us, uc, s[1], c[1]);
-                    rule_row(M - 1, s[M - 2], c[M - 2], ds, dc);
+                    // the last row's rule reads row M-2's H3 of this generation: with
+                    // M = 2 that is row 0's, about to be replaced
+                    const Pl<2> s_up = s[M - 2], c_up = c[M - 2];
+                    if (g + 1 < k) {
+                        h3_row(x[0], s[0], c[0]);
+                        put_top(q);
+                        asm volatile("" ::: "memory");  // progress word after the edge
+                        set_word(prog_top + wv, need + 1u);
+                    }
+                    if (__builtin_amdgcn_readfirstlane((int32_t)(wd - need)) < 0) await(wait_dn, need, pd, td);
+                    Pl<2> ds, dc;
+                    ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
+                    rule_row(M - 1, s_up, c_up, ds, dc);
+                    if (g + 1 < k) {
+                        h3_row(x[M - 1], s[M - 1], c[M - 1]);
+                        put_bot(q);
+                        asm volatile("" ::: "memory");
+                        set_word(prog_bot + wv, need + 1u);
+                    }
                 }
+                __builtin_amdgcn_s_setprio(0);
                 if (g + 1 < k) {
-                    // next generation's H3: the edge rows first, published at once
-                    h3_row(x[0], s[0], c[0]);
-                    if constexpr (M > 1) h3_row(x[M - 1], s[M - 1], c[M - 1]);
-                    put_edges((g + 1) & 1);
-                    asm volatile("" ::: "memory");  // progress word after the edges
-                    if (lane == 0)
-                        __hip_atomic_store(cnt + wv, need + 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
                     for (int i = 1; i < M - 1; ++i) h3_row(x[i], s[i], c[i]);
                 }
-            } else if (g == gmax && lane == 0) {
+            } else if (g == gmax) {
                 // off from here on: release the neighbours for the rest of the epoch
-                __hip_atomic_store(cnt + wv, (uint32_t)(done + k), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                set_word(prog_top + wv, (uint32_t)(done + k));
+                set_word(prog_bot + wv, (uint32_t)(done + k));
             }
         }
 #if GOL_EXP & 2048

@@ -194,3 +194,31 @@ def test_one_waiting_launch_per_device(pkg, oracle):
         grp.step(300)
         got = grp.store_packed()
     assert (got == oracle.bp_run(g, w, 300, oracle.CONWAY, threads=16)).all()
+
+
+def test_waiting_kernel_registry_two_default_engines(pkg, oracle):
+    """Two default engines of one process on one GPU at a hand-off shape (16640 x
+    65536: one-round launches with hand-off blocks when alone), stepped without
+    syncs in between: only the first keeps hand-off blocks (engine.cpp wait
+    registry), both fields exact; a small field created while it lives runs the
+    streaming kernel, and gets the resident kernel again once it is gone."""
+    h, w, gens = 16640, 65536, 48
+    want = oracle.bp_digest(oracle.bp_run(oracle.bp_random(h, w, 5), w, gens, oracle.CONWAY,
+                                          threads=16), w)
+    a = pkg.Engine(h, w, rule=pkg.CONWAY, device=0)
+    b = pkg.Engine(h, w, rule=pkg.CONWAY, device=0)
+    small = pkg.Engine(2048, 4096, rule=pkg.CONWAY, device=0)
+    try:
+        assert a.handoff and not b.handoff, (a.handoff, b.handoff)
+        assert small.resident is None
+        for e in (a, b):
+            e.init_random(5)
+        for _ in range(3):
+            a.step(gens // 3)
+            b.step(gens // 3)
+        assert a.digest() == want and b.digest() == want
+    finally:
+        for e in (a, b, small):
+            e.close()
+    with pkg.Engine(2048, 4096, device=0) as r, pkg.Engine(h, w, device=0) as c:
+        assert r.resident is not None and not c.handoff
