@@ -215,6 +215,7 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     // dev timing build: per-wave cycles waiting for neighbour waves, in epoch
     // hand-offs, and in all (s_memtime), logged at the end
     uint64_t t_wait = 0, t_epoch = 0, t_beg = __builtin_amdgcn_s_memtime(), t_ep0 = 0;
+    uint64_t t_pub = 0, t_flag = 0, t_x = 0;  // epoch pieces: publish + barrier, flag wait + barrier
 #endif
     for (int32_t done = 0; done < a.gens;) {
         const int32_t k = min(a.K, a.gens - done);
@@ -330,6 +331,10 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#if GOL_EXP & 2048
+        t_x = __builtin_amdgcn_s_memtime();
+        t_pub += t_x - t_ep0;
+#endif
         const uint32_t want = a.flag_base + epoch;
         if (threadIdx.x == 0)
             __hip_atomic_store(a.flags + tile, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -349,6 +354,9 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
             }
         }
         __syncthreads();
+#if GOL_EXP & 2048
+        t_flag += __builtin_amdgcn_s_memtime() - t_x;
+#endif
         // reload the halo rows (all lanes) and the halo lanes of the band rows
 #pragma unroll
         for (int i = 0; i < M; ++i) {
@@ -367,11 +375,13 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     }
 #if GOL_EXP & 2048
     if (a.wlog && lane == 0) {
-        uint64_t* wl = a.wlog + ((int64_t)blockIdx.x * W + wv) * 4;
+        uint64_t* wl = a.wlog + ((int64_t)blockIdx.x * W + wv) * 8;
         wl[0] = __builtin_amdgcn_s_memtime() - t_beg;
         wl[1] = t_wait;
         wl[2] = t_epoch;
         wl[3] = (uint64_t)tile << 32 | (uint32_t)gmax;
+        wl[4] = t_pub;
+        wl[5] = t_flag;
     }
 #endif
 }
