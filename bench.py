@@ -28,7 +28,7 @@ prints one JSON line.
     with the best measured rate beside it (profiles/r01/valu_rate.json, 1067 G/s:
     peak_measured, frac_vs_measured);
   * valu.issue_frac: ALL VALU instructions per launch (rocprofv3 SQ_INSTS_VALU
-    of this configuration, committed in profiles/r02/counters.json: warm-up,
+    of this configuration, committed in profiles/r03/counters.json: warm-up,
     masks and halo work included) at the same peak;
   * hbm_equiv_frac: SURVEY §8(d)'s 0.25 B per cell-generation x GCUPS / 8 TB/s
     (> 1 is what temporal blocking buys); hbm_measured_frac: the measured HBM
@@ -99,7 +99,7 @@ def counters_for(cfg):
     record with the same field, rule, depth, streams, GPUs and block kind whose
     rows per wavefront is the same or within 2% (a plan a row or two different
     moves the counters by well under 1%)."""
-    rec = load_json("profiles/r02/counters.json") or {}
+    rec = load_json("profiles/r03/counters.json") or load_json("profiles/r02/counters.json") or {}
     keys = ("size", "rule", "tb_depth", "streams", "n_gpus", "handoff")
     best = None
     for r in rec.get("records", []):
@@ -425,7 +425,8 @@ def main():
                                    if insts else None),
                     "issue_frac_vs_measured": (round(insts * streams / launch_s / meas_slot_rate, 4)
                                                if insts else None),
-                    "counters_from": (f"profiles/r02/counters.json (record of rows_per_wave "
+                    "counters_from": (f"profiles/{ctr.get('source_round', 'r02')}/counters.json "
+                                      f"(record {ctr.get('source')}, rows_per_wave "
                                       f"{ctr.get('rows_per_wave')})" if insts else None),
                 },
                 "hbm_equiv_frac": round(BYTES_PER_CELL_GEN * gcups / HBM_PEAK_GBPS, 4),

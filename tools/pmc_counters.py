@@ -11,7 +11,7 @@
   plus SQ_WAVE_CYCLES, SQ_WAIT_INST_ANY, GRBM_GUI_ACTIVE means, and the mean
   launch time of the dominant stencil instantiation in the bench's kernel trace.
 
-    python tools/pmc_counters.py gpurun_out/prof_r02a --out profiles/r02/counters.json
+    python tools/pmc_counters.py gpurun_out/prof_r03_c3 --out profiles/r03/counters.json
 """
 import argparse
 import csv
@@ -28,8 +28,9 @@ def per_kernel(path, counter):
             continue
         k = r["Kernel_Name"]
         name = "life_tb_kernel" if "life_tb_kernel" in k else (
-            "digest_kernel" if "digest_kernel" in k else (
-                "init_random_kernel" if "init_random_kernel" in k else k))
+            "life_res_kernel" if "life_res_kernel" in k else (
+                "digest_kernel" if "digest_kernel" in k else (
+                    "init_random_kernel" if "init_random_kernel" in k else k)))
         out.setdefault(name, []).append(float(r["Counter_Value"]))
     return out
 
@@ -45,11 +46,13 @@ def config_of(log):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("prof_dir")
-    p.add_argument("--out", default="profiles/r02/counters.json")
+    p.add_argument("--out", default="profiles/r03/counters.json")
     a = p.parse_args()
     d = a.prof_dir
     cfg = config_of(os.path.join(d, "pmc_FETCH_SIZE.log"))
     n, S = cfg["size"], cfg["streams"]
+    kern = cfg.get("kernel", "life_tb_kernel")
+    gpl = cfg.get("gens_per_launch", cfg["tb_depth"])
     fetch = per_kernel(os.path.join(d, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(d, "pmc_WRITE_SIZE", "pmc_counter_collection.csv"), "WRITE_SIZE")
     wq = (n + 63) // 64
@@ -57,42 +60,45 @@ def main():
     # a composite engine runs digest / init per part, over 1/S of the rows each
     f_read = n * wq * 8 / S / (statistics.mean(fetch["digest_kernel"]) * 1024)
     f_write = n * stride * 8 / S / (statistics.mean(write["init_random_kernel"]) * 1024)
-    rd = statistics.mean(fetch["life_tb_kernel"]) * 1024 * f_read
-    wr = statistics.mean(write["life_tb_kernel"]) * 1024 * f_write
+    rd = statistics.mean(fetch[kern]) * 1024 * f_read
+    wr = statistics.mean(write[kern]) * 1024 * f_write
     sq = os.path.join(d, "pmc_sq", "pmc_counter_collection.csv")
     rec = dict(cfg)
-    for k in ("launches", "digest0", "digest"):
+    for k in ("launches", "digest0", "digest", "gens_per_launch"):
         rec.pop(k, None)
     rec.update({
         "hbm_bytes_per_launch": round(rd + wr), "read_bytes_per_launch": round(rd),
         "write_bytes_per_launch": round(wr),
-        "bytes_per_cell_gen_measured": round((rd + wr) * S / (n * n * cfg["tb_depth"]), 5),
+        "bytes_per_cell_gen_measured": round((rd + wr) * S / (n * n * gpl), 5),
+        "gens_per_launch": gpl,
         "fetch_size_calibration": round(f_read, 4), "write_size_calibration": round(f_write, 4),
     })
     if os.path.exists(sq):
         for c in ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
                   "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE", "SQ_INSTS_SALU"):
-            v = per_kernel(sq, c).get("life_tb_kernel")
+            v = per_kernel(sq, c).get(kern)
             if v:
                 rec[c.lower() + "_per_launch"] = round(statistics.mean(v))
         rec["insts_valu_per_launch"] = rec.get("sq_insts_valu_per_launch")
-        rec["launches_profiled"] = len(per_kernel(sq, "SQ_INSTS_VALU").get("life_tb_kernel", []))
+        rec["launches_profiled"] = len(per_kernel(sq, "SQ_INSTS_VALU").get(kern, []))
     stats = glob.glob(os.path.join(d, "trace", "*kernel_stats.csv"))
     if stats:  # the bench command's kernel trace: the dominant stencil instantiation
-        rows = [r for r in csv.DictReader(open(stats[0])) if "life_tb_kernel" in r["Name"]]
+        rows = [r for r in csv.DictReader(open(stats[0])) if kern in r["Name"]]
         if rows:
             top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
             rec["trace_kernel"] = top["Name"]
             rec["trace_avg_launch_ns"] = float(top["AverageNs"])
             rec["trace_calls"] = int(top["Calls"])
     rec["source"] = os.path.basename(os.path.normpath(d))
+    rec["source_round"] = os.path.basename(os.path.dirname(os.path.abspath(a.out)))
     doc = {"records": []}
     if os.path.exists(a.out):
         doc = json.load(open(a.out))
     keys = ("size", "rule", "tb_depth", "streams", "n_gpus", "rows_per_wave", "handoff")
     doc["records"] = [r for r in doc["records"] if not all(r.get(k) == rec[k] for k in keys)]
     doc["records"].append(rec)
-    doc["_doc"] = ("Per-launch counters of life_tb_kernel by configuration: rocprofv3 --pmc "
+    doc["_doc"] = ("Per-launch counters of the stencil kernel (life_tb_kernel, or life_res_kernel "
+                   "for resident fields) by configuration: rocprofv3 --pmc "
                    "passes (FETCH_SIZE, WRITE_SIZE and the SQ set each in its own run) over "
                    "tools/profile_run.py; see tools/pmc_counters.py")
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

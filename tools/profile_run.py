@@ -7,7 +7,9 @@ uncalibrated for widths other than 16 B/lane).
 
   init_random_kernel : writes exactly rows*stride*8 bytes (8 B/lane stores)
   digest_kernel      : reads exactly rows*wq*8 bytes (8 B/lane loads)
-  life_tb_kernel     : `launches` x tb_depth generations of the field
+  life_tb_kernel     : `launches` x tb_depth generations of the field (or, for a
+                       field the resident kernel takes, `launches` launches of
+                       `gens` generations: life_res_kernel)
 
 Prints one JSON line with the engine's configuration (bench.py's record keys),
 which tools/pmc_counters.py reads back.
@@ -28,6 +30,8 @@ p.add_argument("--rows-per-wave", type=int, default=0)
 p.add_argument("--handoff", type=int, default=0)
 p.add_argument("--streams", type=int, default=0)
 p.add_argument("--launches", type=int, default=16)
+p.add_argument("--gens", type=int, default=1000,
+               help="resident engines: generations per launch (one launch per gol_step)")
 a = p.parse_args()
 pkg = entry.load_package()
 rule = pkg.REF_RULE if a.rule == "ref" else pkg.CONWAY
@@ -36,11 +40,19 @@ e = pkg.Engine(a.size, a.size, rule=rule, device=0, tb_depth=a.tb_depth,
 e.init_random(1)
 d0 = e.digest()
 e.set_timing(1)
-e.step(e.tb_depth * a.launches)
+if e.resident:  # the bench's launches: one per gol_step of `gens` generations
+    for _ in range(a.launches):
+        e.step(a.gens)
+    gens_per_launch = a.gens
+else:
+    e.step(e.tb_depth * a.launches)
+    gens_per_launch = e.tb_depth
 e.sync()
 tm = e.timing()
 print(json.dumps({"size": a.size, "rule": a.rule, "tb_depth": e.tb_depth,
                   "streams": max(1, tm["streams"]), "n_gpus": 1,
                   "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
+                  "kernel": "life_res_kernel" if e.resident else "life_tb_kernel",
+                  "gens_per_launch": gens_per_launch,
                   "launches": tm["launches"], "digest0": d0, "digest": e.digest()}))
 e.close()
