@@ -743,8 +743,15 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     const uint64_t minR = h / (uint64_t)nranks;
     if (minR == 0) return fail(GOL_EINVAL, "fewer rows than ranks");
     g->K = auto_layout(g->R, cfg).K;
-    // rounds of halo_depth generations between exchanges (default 8 launches)
-    uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : 8 * (uint64_t)g->K;
+    // Rounds of halo_depth generations between exchanges: 8 launches, or 16 for
+    // K = 16 stripes of at most 12288 rows.  Per-rank proxy over the RCCL byte mover
+    // (self-loop communicator, tools/rank_proxy.py, profiles/r03/rank_proxy_rccl.jsonl):
+    // the 8-way 65536^2 rank (8192 rows) ran 107.8 TCUPS at Hx = 128 and 109.3 at
+    // 256 -- half the rounds, each with an exchange and a launch sequence whose
+    // first, longest launch fits the one-round plans worst -- against 1.6% more halo
+    // rows; the 4-way rank was 117.2 at 128 and 116.5-116.7 at 192-256.
+    const uint64_t launches_per_round = (g->K >= 16 && g->R <= 12288) ? 16 : 8;
+    uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : launches_per_round * (uint64_t)g->K;
     if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
     g->Hx = nranks > 1 ? Hx : 0;
     g->raw.clear();

@@ -162,10 +162,20 @@ def test_rank_protocol_from_engine_schedule(oracle, monkeypatch, world, K, Hx, c
     assert (got == ref_cells).all()
 
 
+def test_default_halo_depth(pkg):
+    """Rounds of 8 launches, 16 for K = 16 stripes of at most 12288 rows (the 8-way
+    65536^2 rank: engine.cpp rank_geometry)."""
+    for nranks, want in ((2, 128), (4, 128), (8, 256)):
+        _, K, Hx = pkg.round_schedule(65536, 65536, 1, nranks, 16)
+        assert (K, Hx) == (16, want), nranks
+    _, K, Hx = pkg.round_schedule(1200, 2000, 0, 2, 16, tb_depth=8)
+    assert (K, Hx) == (8, 64)
+
+
 def test_schedule_structure_default(pkg):
-    """A rank engine's default schedule for the C4 8-rank stripe: rounds of Hx =
-    128 generations (eight 16-deep launches) between blocking exchanges."""
-    ops, K, Hx = pkg.round_schedule(65536, 65536, 3, 8, 300)
+    """A rank engine's blocking schedule for the C4 8-rank stripe at Hx = 128:
+    rounds of eight 16-deep launches between blocking exchanges."""
+    ops, K, Hx = pkg.round_schedule(65536, 65536, 3, 8, 300, halo_depth=128)
     assert (K, Hx) == (16, 128)
     kinds = [pkg.OP_NAMES[o["kind"]] for o in ops]
     assert kinds[:18] == (["EXCHANGE"] + ["LAUNCH"] * 8) * 2
@@ -179,7 +189,7 @@ def test_schedule_structure(pkg, monkeypatch):
     round ends in band + interior + overlapped exchange, and the next call starts
     from that exchange."""
     monkeypatch.setenv("GOL_DEV_OVERLAP", "1")
-    ops, K, Hx = pkg.round_schedule(65536, 65536, 3, 8, 300)
+    ops, K, Hx = pkg.round_schedule(65536, 65536, 3, 8, 300, halo_depth=128)
     assert (K, Hx) == (16, 128)
     kinds = [pkg.OP_NAMES[o["kind"]] for o in ops]
     assert kinds[0] == "EXCHANGE"
@@ -189,10 +199,11 @@ def test_schedule_structure(pkg, monkeypatch):
     assert ops[8]["segs"] == [(128, 256), (8192, 8320)]  # rows the neighbours need
     assert ops[9]["segs"] == [(256, 8192)]
     assert ops[-1]["kind"] == pkg.OP_LAUNCH and sum(o["depth"] for o in ops[-4:]) == 300 - 256
-    fresh_ops, _, _ = pkg.round_schedule(65536, 65536, 3, 8, 128, halo_fresh=True)
+    fresh_ops, _, _ = pkg.round_schedule(65536, 65536, 3, 8, 128, halo_fresh=True,
+                                         halo_depth=128)
     assert fresh_ops[0]["kind"] == pkg.OP_WAIT_EXCHANGE
     # top and bottom ranks have one band segment, and no overlap when R < 2 Hx
-    top, _, _ = pkg.round_schedule(65536, 65536, 0, 8, 128)
+    top, _, _ = pkg.round_schedule(65536, 65536, 0, 8, 128, halo_depth=128)
     assert [o["segs"] for o in top if o["kind"] == pkg.OP_BAND] == [[(8192, 8320)]]
     small, _, hx = pkg.round_schedule(100, 64, 0, 2, 50, halo_depth=40)
     assert hx == 40 and pkg.OP_BAND not in [o["kind"] for o in small]

@@ -53,7 +53,7 @@ def mirrored_steps(oracle, own, w, chunks, rule, Hx, has_up, has_dn):
     (2, 0, 8, 32, "conway"),     # bottom neighbour only
     (2, 1, 16, 64, "conway"),    # top neighbour only
     (3, 1, 8, 24, "highlife"),   # both
-    (4, 2, 16, 0, "ref"),        # both, default halo depth (8K)
+    (4, 2, 16, 0, "ref"),        # both, default halo depth
 ])
 def test_rccl_self_loop(pkg, oracle, monkeypatch, world, rank, K, Hx, rule, overlap):
     """overlap 1: blocking exchanges on the compute stream; 2: the band launch,
@@ -99,16 +99,16 @@ def test_rccl_self_loop(pkg, oracle, monkeypatch, world, rank, K, Hx, rule, over
 
 
 def test_rccl_self_loop_c4_rank_shape(pkg, monkeypatch):
-    """The 8-way C4 per-rank shape (8192 own rows of 65536^2 + 2 x 128 halo rows,
-    default K = 16, age-skewed one-round launches, default block kind): 1 MiB
+    """The 8-way C4 per-rank shape (8192 own rows of 65536^2 + 2 x 256 halo rows,
+    default K = 16, age-skewed one-round launches, default block kind): 2 MiB
     messages through RCCL every round, bytewise equal to the host loopback."""
     monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
-    n, world, rank, gens = 65536, 8, 3, 2 * 128 + 40
+    n, world, rank, gens = 65536, 8, 3, 2 * 256 + 40
     out = []
     for mode in ("rccl", "host"):
         kw = dict(uid=pkg.unique_id()) if mode == "rccl" else dict(transport=lambda su, sd: (su, sd))
         with pkg.Engine(n, n, rule=pkg.CONWAY, device=0, rank=rank, nranks=world, **kw) as e:
-            assert e.halo_depth == 128
+            assert e.halo_depth == 256
             e.init_random(3)
             e.step(gens)
             out.append((e.digest(), e.store_packed()))

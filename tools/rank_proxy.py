@@ -6,13 +6,18 @@ of that split (the slowest kind: a middle rank, halos on both sides) runs alone 
 the GPU with a host transport that moves no rows (the B/S2 stencil's cost does not
 depend on the data), through the
 same schedule: Hx-generation rounds, shrinking launches, band + interior split
-with the exchange on its own stream.  The transport is a native no-op: the
-engine still stages the halo rows through pinned host memory and waits for the
-band launch on the host each round (which RCCL does not), but no bytes move
-(1 MiB per neighbour and round at 65536^2 over RCCL).  Prints per-rank TCUPS (own rows)
-and the aggregate N x rate a perfectly balanced job would report.
+with the exchange on its own stream.  Transports (--transports):
+  * noop: a native host transport that moves nothing: the engine still stages
+    the halo rows through pinned host memory and waits for the band launch on the
+    host each round (which RCCL does not);
+  * rccl: the RCCL byte mover itself against a self-loop communicator
+    (GOL_DEV_RCCL_SELF=1): RCCL's kernels and stream ordering are paid, the
+    1 MiB per neighbour and round move as device-local copies instead of over xGMI.
+Prints per-rank TCUPS (own rows) and the aggregate N x rate a perfectly balanced
+job would report.
 
-    python tools/rank_proxy.py [--size 65536] [--ranks 2,4,8] [--skews auto,0]
+    python tools/rank_proxy.py [--size 65536] [--ranks 2,4,8] [--skews auto,0] \
+        [--transports noop,rccl] [--overlaps 1,2]
 """
 import argparse
 import json
@@ -50,9 +55,17 @@ def noop_transport(pkg):
     return pkg.Transport(fn, None), (lib, fn)
 
 
-def rank_engine(pkg, n, rank, nranks, tp, handoff=0):
+def rank_engine(pkg, n, rank, nranks, tp, handoff=0, overlap=0, transport="noop", hx=0):
     import ctypes
-    cfg = pkg.make_config(pkg.REF_RULE, 0, pkg.SEM_GLOBAL, 1, 0, 0, 0, handoff, 0, 0, 0, 0)
+    if transport == "rccl":
+        os.environ["GOL_DEV_RCCL_SELF"] = "1"
+        try:
+            return pkg.Engine(n, n, device=0, rank=rank, nranks=nranks, uid=pkg.unique_id(),
+                              handoff=handoff, exchange_overlap=overlap, halo_depth=hx)
+        finally:
+            os.environ.pop("GOL_DEV_RCCL_SELF", None)
+    cfg = pkg.make_config(pkg.REF_RULE, 0, pkg.SEM_GLOBAL, 1, 0, hx, 0, handoff, 0, 0, 0, 0,
+                          exchange_overlap=overlap)
     h = ctypes.c_void_p()
     pkg._check(pkg.lib().gol_create_rank_transport(n, n, ctypes.byref(cfg), rank, nranks,
                                                    ctypes.byref(tp), ctypes.byref(h)))
@@ -67,7 +80,10 @@ def main():
     p.add_argument("--gens", type=int, default=1000)
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--handoff", type=int, default=0, help="gol_config.handoff")
-    p.add_argument("--overlaps", default="default", help="GOL_DEV_OVERLAP values (default = unset)")
+    p.add_argument("--overlaps", default="0", help="gol_config.exchange_overlap values "
+                   "(0 auto = blocking for rank engines, 1 blocking, 2 overlapped)")
+    p.add_argument("--transports", default="noop", help="noop and/or rccl (self-loop)")
+    p.add_argument("--halo-depths", default="0", help="gol_config.halo_depth values (0 = auto)")
     a = p.parse_args()
     pkg = entry.load_package()
     n = a.size
@@ -75,23 +91,20 @@ def main():
     for N in (int(x) for x in a.ranks.split(",")):
         rank = N // 2
         engines = []
-        for ov in a.overlaps.split(","):
-            for sk in a.skews.split(","):
-                if sk == "auto":
-                    os.environ.pop("GOL_DEV_AGE_SKEW", None)
-                else:
-                    os.environ["GOL_DEV_AGE_SKEW"] = sk
-                if ov == "default":
-                    os.environ.pop("GOL_DEV_OVERLAP", None)
-                else:
-                    os.environ["GOL_DEV_OVERLAP"] = ov
-                e = rank_engine(pkg, n, rank, N, tp, a.handoff)
-                e.init_random(1)
-                e.step(a.gens)
-                e.sync()
-                engines.append(((sk, ov), e, []))
+        for trn in a.transports.split(","):
+            for ov in (int(x) for x in a.overlaps.split(",")):
+                for hx in (int(x) for x in a.halo_depths.split(",")):
+                    for sk in a.skews.split(","):
+                        if sk == "auto":
+                            os.environ.pop("GOL_DEV_AGE_SKEW", None)
+                        else:
+                            os.environ["GOL_DEV_AGE_SKEW"] = sk
+                        e = rank_engine(pkg, n, rank, N, tp, a.handoff, ov, trn, hx)
+                        e.init_random(1)
+                        e.step(a.gens)
+                        e.sync()
+                        engines.append(((sk, ov, trn), e, []))
         os.environ.pop("GOL_DEV_AGE_SKEW", None)
-        os.environ.pop("GOL_DEV_OVERLAP", None)
         for _ in range(a.rounds):
             for sk, e, ts in engines:
                 t0 = time.perf_counter()
@@ -105,6 +118,7 @@ def main():
                               "halo_depth": e.halo_depth, "tb_depth": e.tb_depth,
                               "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
                               "age_skew": e.age_skew, "skew_cfg": sk[0], "overlap_cfg": sk[1],
+                              "transport": sk[2],
                               "rank_tcups": round(rate, 2),
                               "aggregate_tcups_if_balanced": round(rate * N, 1),
                               "ms_per_1000_gens": round(t * 1e3 * 1000 / a.gens, 2)}), flush=True)
