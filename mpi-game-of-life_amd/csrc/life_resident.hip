@@ -199,8 +199,9 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     // spin until *p >= need (after a first read that came back short), then re-read
     // the edge: progress read before edge read, LDS in order per wave
     auto await = [&](uint32_t* p, uint32_t need, const uint4* pe, uint4& t) {
-        for (int n = 0;; ++n) {
-            if (n > kPollLimit) {  // lost: flag it, go on so the launch drains
+        const uint64_t t0 = wait_clock();
+        for (;;) {
+            if (wait_clock() - t0 > kWaitTicks) {  // lost: flag it, go on so the launch drains
                 __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
@@ -341,11 +342,13 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
         if (done >= a.gens) break;
         // wait for the neighbours' rows of this epoch
         if (nb_tile >= 0 && !gave_up && !(GOL_EXP & 64)) {
-            int n = 0;
-            while ((int32_t)(__hip_atomic_load(a.flags + nb_tile, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) -
-                             want) < 0) {
-                if (++n > kPollLimit) {  // the field is lost: flag it, stop waiting
+            uint64_t t0 = 0;
+            for (int n = 0; (int32_t)(__hip_atomic_load(a.flags + nb_tile, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT) -
+                                      want) < 0;
+                 ++n) {
+                if (n == 0) t0 = wait_clock();
+                else if (wait_clock() - t0 > kWaitTicks) {  // the field is lost: flag it, stop waiting
                     __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     gave_up = true;
                     break;

@@ -300,10 +300,13 @@ __device__ __forceinline__ void place_block(Pl<NP> (&x)[PF])
 #undef GOL_PL2
 #undef GOL_PL4
 
-// Upper bound of a hand-off wait: polls of ~1 us each (the producer normally
-// finished its first rows long before), then give up, flag the error and go on
-// so that the launch always drains.
-constexpr int kPollLimit = 1 << 16;
+// Upper bound of a wait for another wavefront (hand-off rows, resident tiles and
+// waves): 2 s of the 100 MHz constant clock (s_memrealtime), read only while the
+// awaited value is not there yet.  A wait that long means the protocol is broken
+// (or the GPU is shared with something that holds it for seconds): flag the
+// error and go on, so that the launch always drains and gol_sync reports it.
+constexpr uint64_t kWaitTicks = 200000000ull;
+__device__ __forceinline__ uint64_t wait_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
 // Block modes of the stencil kernel (see `block`).
 constexpr int kWarmBlk = 0, kPure = 1, kSide = 2;
@@ -507,11 +510,14 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     auto wait_below = [&]() {
         const uint32_t* f = a.flags + (unit - a.strips);
         uint32_t v = 0;
-        for (int it = 0; it < ((GOL_EXP & 1) ? 0 : kPollLimit); ++it) {
+        uint64_t t0 = 0;
+        for (int it = 0; !(GOL_EXP & 1); ++it) {
             v = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT));
             if (v) break;
+            if (it == 0) t0 = wait_clock();
+            else if (wait_clock() - t0 > kWaitTicks) break;
             __builtin_amdgcn_s_sleep(8);
         }
         if (lane == 0) {
