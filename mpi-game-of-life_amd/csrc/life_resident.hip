@@ -52,7 +52,7 @@ namespace {
 // (profiles/r03/c2_tiles_per_cu.txt).
 constexpr int kResEdgeWords = 2 * 2 * kResWaves * 64 * 2;
 constexpr int kResLdsWords = 96 * 1024 / 8;
-static_assert(kResEdgeWords + 128 + kResWaves <= kResLdsWords,
+static_assert(kResEdgeWords + 128 + kResWaves * 64 <= kResLdsWords,
               "edge H3 rows, the zero row and the progress words fit the LDS block");
 
 // H3 of a row: bit-sliced sum (s) and carry (c) of each cell and its 2
@@ -166,10 +166,11 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     // after the edge slots: a zero row (the edges of the missing neighbours of the
     // first and last wave), then two progress words per wave: the top / bottom
     // edge of generation n of the launch is in its slot once top[wave] / bot[wave]
-    // >= n
+    // >= n.  Every lane stores the word into a slot of its own (one conflict-free
+    // store, no lane-0 branch); readers read slot 0.
     uint4* const zero4 = ed4 + 4 * W * 64;
     uint32_t* const prog_top = reinterpret_cast<uint32_t*>(zero4 + 64);
-    uint32_t* const prog_bot = prog_top + W;
+    uint32_t* const prog_bot = prog_top + W * 64;
     if (wv == 0) zero4[lane] = uint4{0u, 0u, 0u, 0u};
     auto rule_row = [&](int i, const Pl<2>& as, const Pl<2>& ac, const Pl<2>& es,
                         const Pl<2>& ec) {
@@ -188,13 +189,15 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     const int32_t gmax = (int32_t)min<int64_t>(r0 + M - (b0 - a.K) - 1, b1 + a.K - 1 - r0);
     const bool has_up = wv > 0, has_dn = wv < W - 1;
     // the first / last wave waits on its own word (always current) instead
-    uint32_t* const wait_up = has_up ? prog_bot + wv - 1 : prog_top + wv;
-    uint32_t* const wait_dn = has_dn ? prog_top + wv + 1 : prog_bot + wv;
+    uint32_t* const wait_up = has_up ? prog_bot + (wv - 1) * 64 : prog_top + wv * 64;
+    uint32_t* const wait_dn = has_dn ? prog_top + (wv + 1) * 64 : prog_bot + wv * 64;
+    uint32_t* const my_top = prog_top + wv * 64 + lane;
+    uint32_t* const my_bot = prog_bot + wv * 64 + lane;
     auto word = [](uint32_t* p) {
         return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     auto set_word = [&](uint32_t* p, uint32_t v) {
-        if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     // spin until *p >= need (after a first read that came back short), then re-read
     // the edge: progress read before edge read, LDS in order per wave
@@ -225,8 +228,8 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
         put_top(0);
         put_bot(0);
         // (a wave whose rows are never exact this epoch releases its neighbours now)
-        set_word(prog_top + wv, (uint32_t)(gmax > 0 ? done : done + k));
-        set_word(prog_bot + wv, (uint32_t)(gmax > 0 ? done : done + k));
+        set_word(my_top, (uint32_t)(gmax > 0 ? done : done + k));
+        set_word(my_bot, (uint32_t)(gmax > 0 ? done : done + k));
         __syncthreads();
         // Generations: no workgroup barrier.  A wave's first row needs the upper
         // neighbour wave's bottom edge, its last row the lower neighbour's top edge;
@@ -239,82 +242,87 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
         // and read after it.  An edge slot is rewritten two generations later, after
         // the wave that reads it has raised the word it publishes after that read
         // (which this wave waits for before computing the row).
-        for (int32_t g = 0; g < k; ++g) {
-            if (g < gmax) {
-                const uint32_t need = (uint32_t)(done + g);
-                const int p = g & 1, q = (g + 1) & 1;
-                const uint4* pu = has_up ? ed4 + p * (2 * W * 64) + (W + wv - 1) * 64 + lane : zero4 + lane;
-                const uint4* pd = has_dn ? ed4 + p * (2 * W * 64) + (wv + 1) * 64 + lane : zero4 + lane;
+        // generation g of the epoch (g < gmax); `publish`: not the epoch's last
+        auto generation = [&](int32_t g, bool publish) {
+            const uint32_t need = (uint32_t)(done + g);
+            const int p = g & 1, q = (g + 1) & 1;
+            const uint4* pu = has_up ? ed4 + p * (2 * W * 64) + (W + wv - 1) * 64 + lane : zero4 + lane;
+            const uint4* pd = has_dn ? ed4 + p * (2 * W * 64) + (wv + 1) * 64 + lane : zero4 + lane;
 #if GOL_EXP & 2048
-                const uint64_t tw0 = __builtin_amdgcn_s_memtime();
+            const uint64_t tw0 = __builtin_amdgcn_s_memtime();
 #endif
-                const uint32_t wu = word(wait_up), wd = word(wait_dn);
-                asm volatile("" ::: "memory");  // edge reads issue after the progress reads
-                uint4 tu = *pu, td = *pd;
-                // interior rows first: no LDS operand, they cover the round trip
+            const uint32_t wu = word(wait_up), wd = word(wait_dn);
+            asm volatile("" ::: "memory");  // edge reads issue after the progress reads
+            uint4 tu = *pu, td = *pd;
+            // interior rows first: no LDS operand, they cover the round trip
 #pragma unroll
-                for (int i = 1; i < M - 1; ++i) {
-                    rule_row(i, s[i - 1], c[i - 1], s[i + 1], c[i + 1]);
-                    asm volatile("" : "+v"(x[i].v[0]), "+v"(x[i].v[1]));
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (__builtin_amdgcn_readfirstlane((int32_t)(wu - need)) < 0) await(wait_up, need, pu, tu);
-#if GOL_EXP & 2048
-                {
-                    uint32_t v = tu.x;
-                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
-                    t_wait += __builtin_amdgcn_s_memtime() - tw0;
-                    if (v == 0x5a5a5a5au) tu.y ^= 1u;  // keeps v live (never taken on real data)
-                }
-#endif
-                __builtin_amdgcn_s_setprio(2);
-                Pl<2> us, uc;
-                us.v[0] = tu.x; us.v[1] = tu.y; uc.v[0] = tu.z; uc.v[1] = tu.w;
-                if constexpr (M == 1) {
-                    if (__builtin_amdgcn_readfirstlane((int32_t)(wd - need)) < 0) await(wait_dn, need, pd, td);
-                    Pl<2> ds, dc;
-                    ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
-                    rule_row(0, us, uc, ds, dc);
-                    if (g + 1 < k) {
-                        h3_row(x[0], s[0], c[0]);
-                        put_top(q);
-                        put_bot(q);
-                        asm volatile("" ::: "memory");  // progress words after the edges
-                        set_word(prog_top + wv, need + 1u);
-                        set_word(prog_bot + wv, need + 1u);
-                    }
-                } else {
-                    rule_row(0, us, uc, s[1], c[1]);
-                    // the last row's rule reads row M-2's H3 of this generation: with
-                    // M = 2 that is row 0's, about to be replaced
-                    const Pl<2> s_up = s[M - 2], c_up = c[M - 2];
-                    if (g + 1 < k) {
-                        h3_row(x[0], s[0], c[0]);
-                        put_top(q);
-                        asm volatile("" ::: "memory");  // progress word after the edge
-                        set_word(prog_top + wv, need + 1u);
-                    }
-                    if (__builtin_amdgcn_readfirstlane((int32_t)(wd - need)) < 0) await(wait_dn, need, pd, td);
-                    Pl<2> ds, dc;
-                    ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
-                    rule_row(M - 1, s_up, c_up, ds, dc);
-                    if (g + 1 < k) {
-                        h3_row(x[M - 1], s[M - 1], c[M - 1]);
-                        put_bot(q);
-                        asm volatile("" ::: "memory");
-                        set_word(prog_bot + wv, need + 1u);
-                    }
-                }
-                __builtin_amdgcn_s_setprio(0);
-                if (g + 1 < k) {
-#pragma unroll
-                    for (int i = 1; i < M - 1; ++i) h3_row(x[i], s[i], c[i]);
-                }
-            } else if (g == gmax) {
-                // off from here on: release the neighbours for the rest of the epoch
-                set_word(prog_top + wv, (uint32_t)(done + k));
-                set_word(prog_bot + wv, (uint32_t)(done + k));
+            for (int i = 1; i < M - 1; ++i) {
+                rule_row(i, s[i - 1], c[i - 1], s[i + 1], c[i + 1]);
+                asm volatile("" : "+v"(x[i].v[0]), "+v"(x[i].v[1]));
             }
+            __builtin_amdgcn_sched_barrier(0);
+            if (__builtin_amdgcn_readfirstlane((int32_t)(wu - need)) < 0) await(wait_up, need, pu, tu);
+#if GOL_EXP & 2048
+            {
+                uint32_t v = tu.x;
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
+                t_wait += __builtin_amdgcn_s_memtime() - tw0;
+                if (v == 0x5a5a5a5au) tu.y ^= 1u;  // keeps v live (never taken on real data)
+            }
+#endif
+            __builtin_amdgcn_s_setprio(2);
+            Pl<2> us, uc;
+            us.v[0] = tu.x; us.v[1] = tu.y; uc.v[0] = tu.z; uc.v[1] = tu.w;
+            if constexpr (M == 1) {
+                if (__builtin_amdgcn_readfirstlane((int32_t)(wd - need)) < 0) await(wait_dn, need, pd, td);
+                Pl<2> ds, dc;
+                ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
+                rule_row(0, us, uc, ds, dc);
+                if (publish) {
+                    h3_row(x[0], s[0], c[0]);
+                    put_top(q);
+                    put_bot(q);
+                    asm volatile("" ::: "memory");  // progress words after the edges
+                    set_word(my_top, need + 1u);
+                    set_word(my_bot, need + 1u);
+                }
+            } else {
+                rule_row(0, us, uc, s[1], c[1]);
+                // the last row's rule reads row M-2's H3 of this generation: with
+                // M = 2 that is row 0's, about to be replaced
+                const Pl<2> s_up = s[M - 2], c_up = c[M - 2];
+                if (publish) {
+                    h3_row(x[0], s[0], c[0]);
+                    put_top(q);
+                    asm volatile("" ::: "memory");  // progress word after the edge
+                    set_word(my_top, need + 1u);
+                }
+                if (__builtin_amdgcn_readfirstlane((int32_t)(wd - need)) < 0) await(wait_dn, need, pd, td);
+                Pl<2> ds, dc;
+                ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
+                rule_row(M - 1, s_up, c_up, ds, dc);
+                if (publish) {
+                    h3_row(x[M - 1], s[M - 1], c[M - 1]);
+                    put_bot(q);
+                    asm volatile("" ::: "memory");
+                    set_word(my_bot, need + 1u);
+                }
+            }
+            __builtin_amdgcn_s_setprio(0);
+            if (publish) {
+#pragma unroll
+                for (int i = 1; i < M - 1; ++i) h3_row(x[i], s[i], c[i]);
+            }
+        };
+        // this wave computes generations [0, gend) of the epoch; the last one it
+        // computes publishes its edges unless it is the epoch's last
+        const int32_t gend = min(k, gmax);
+        for (int32_t g = 0; g < gend - 1; ++g) generation(g, true);
+        if (gend > 0) generation(gend - 1, gend < k);
+        if (gend < k) {
+            // off from here on: release the neighbours for the rest of the epoch
+            set_word(my_top, (uint32_t)(done + k));
+            set_word(my_bot, (uint32_t)(done + k));
         }
 #if GOL_EXP & 2048
         t_ep0 = __builtin_amdgcn_s_memtime();

@@ -8,7 +8,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_
     > $OUT/tests.log 2>&1 || { grep -E "FAILED|Error|passed|failed" $OUT/tests.log | head -20; exit 2; }
 tail -1 $OUT/tests.log
 for rep in 1 2 3; do
-  for lib in libgol.so libgol_prio.so libgol_r02.so; do
+  for lib in libgol.so libgol_split.so libgol_prio.so; do
     for rule in ref conway; do
       GOL_LIB=mpi-game-of-life_amd/$lib timeout -k 10 60 python3 tools/profile_resident.py --steps 5 --rule $rule 2>/dev/null | sed "s/^/$lib /" >> $OUT/ab.log || exit 5
     done
