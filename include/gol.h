@@ -70,7 +70,9 @@ typedef struct gol_config {
     uint32_t ref_ranks;    /* P for GOL_SEM_REF_STRIPES (must satisfy h >= P) */
     uint32_t tb_depth;     /* generations fused per kernel launch (temporal
                               blocking); 0 = auto; allowed 1,2,4,6,7,8,12,16
-                              (the dev build, make dev, adds 20,24,32) */
+                              (the dev build, make dev, adds 20,24,32); with
+                              resident = 2, the resident kernel's epoch length,
+                              any of 1..63 */
     uint32_t halo_depth;   /* multi-rank: halo rows exchanged per round
                               (= generations between exchanges); 0 = auto */
     uint32_t rows_per_wave;/* rows each wavefront streams per launch; 0 = auto */

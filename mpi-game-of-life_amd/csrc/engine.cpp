@@ -710,8 +710,10 @@ gol_status check_cfg(const gol_config* cfg)
     if (!cfg) return fail(GOL_EINVAL, "null config");
     if (cfg->birth_mask >= 512 || cfg->survive_mask >= 512)
         return fail(GOL_EINVAL, "rule masks must be 9-bit");
-    if (cfg->tb_depth != 0 && std::find(std::begin(gol::kDepthList), std::end(gol::kDepthList),
-                                        (int)cfg->tb_depth) == std::end(gol::kDepthList))
+    // (the resident kernel takes any epoch length K <= 63: resident = 2 with tb_depth)
+    if (cfg->tb_depth != 0 && !(cfg->resident == 2 && cfg->tb_depth <= 63) &&
+        std::find(std::begin(gol::kDepthList), std::end(gol::kDepthList),
+                  (int)cfg->tb_depth) == std::end(gol::kDepthList))
         return fail(GOL_EINVAL, gol::kDevKernels
                                     ? "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16,20,24,32"
                                     : "tb_depth must be 0 (auto) or one of 1,2,4,6,7,8,12,16 "
@@ -934,6 +936,9 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->rule = gol::RULE_GENERIC;
     const Layout lay = auto_layout(e->R, cfg);
     e->K = lay.K;
+    // a resident epoch length with no streaming kernel of that depth: the
+    // streaming plans (never launched while the resident kernel runs) use 16
+    if (cfg->resident == 2 && !gol::life_has_kernel((int)e->K, lay.planes)) e->K = 16;
     e->rows_per_wave = cfg->rows_per_wave;
     e->lane_shift = cfg->strip_lanes == 64 ? 0 : cfg->strip_lanes == 32 ? 1
                   : cfg->strip_lanes == 16 ? 2 : -1;
