@@ -7,7 +7,7 @@ field buffers every K generations under sc1 flags.  Bit-exact bar, every call
 through the C ABI.  Covers: one strip with all 64 lanes as field groups and
 multi-strip rows (62 groups + halo lanes, corner neighbours), partial last
 bands, every rows-per-wavefront instantiation, K from 1 to the largest that
-fits, rules without and with births (B0 included: the dead border and columns
+fits (including epoch lengths with no streaming instantiation), rules without and with births (B0 included: the dead border and columns
 beyond w must stay masked), flag counts carried across launches, odd/even
 epoch counts (buffer parity), and the hand-off under uneven load.
 """
@@ -38,7 +38,9 @@ def test_resident_random_fields(pkg, oracle, shape, rule):
     g = oracle.bp_random(h, w, seed)
     want = {n: oracle.bp_run(g, w, n, R) for n in (1, 3, 16, 21, 70)}
     for cfg in ({}, {"rows_per_wave": 2, "tb_depth": 1}, {"rows_per_wave": 3, "tb_depth": 7},
-                {"rows_per_wave": 8, "tb_depth": 16}):
+                {"rows_per_wave": 8, "tb_depth": 16},
+                # epoch lengths the streaming kernel does not instantiate
+                {"rows_per_wave": 4, "tb_depth": 22}, {"rows_per_wave": 6, "tb_depth": 5}):
         try:
             e = pkg.Engine(h, w, rule=R, device=0, resident=2, **cfg)
         except pkg.GolError:
