@@ -251,6 +251,16 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
 #if GOL_EXP & 2048
             const uint64_t tw0 = __builtin_amdgcn_s_memtime();
 #endif
+#if GOL_EXP & 4096
+            // dev trace (tools/res_trace.py): shader-clock stamps per generation
+            uint64_t ts[5];
+            auto stamp = [&](int j) { ts[j] = __builtin_amdgcn_s_memtime(); };
+            auto stamp_on = [&](int j, uint32_t& v) {
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
+                ts[j] = __builtin_amdgcn_s_memtime();
+            };
+            stamp(0);
+#endif
             const uint32_t wu = word(wait_up), wd = word(wait_dn);
             asm volatile("" ::: "memory");  // edge reads issue after the progress reads
             uint4 tu = *pu, td = *pd;
@@ -269,6 +279,9 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
                 t_wait += __builtin_amdgcn_s_memtime() - tw0;
                 if (v == 0x5a5a5a5au) tu.y ^= 1u;  // keeps v live (never taken on real data)
             }
+#endif
+#if GOL_EXP & 4096
+            stamp_on(1, tu.x);
 #endif
             __builtin_amdgcn_s_setprio(2);
             Pl<2> us, uc;
@@ -297,7 +310,13 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
                     asm volatile("" ::: "memory");  // progress word after the edge
                     set_word(my_top, need + 1u);
                 }
+#if GOL_EXP & 4096
+                stamp(2);
+#endif
                 if (__builtin_amdgcn_readfirstlane((int32_t)(wd - need)) < 0) await(wait_dn, need, pd, td);
+#if GOL_EXP & 4096
+                stamp_on(3, td.x);
+#endif
                 Pl<2> ds, dc;
                 ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
                 rule_row(M - 1, s_up, c_up, ds, dc);
@@ -307,6 +326,17 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
                     asm volatile("" ::: "memory");
                     set_word(my_bot, need + 1u);
                 }
+#if GOL_EXP & 4096
+                stamp(4);
+                // per-generation trace of the middle tile, generations 32..95
+                const int32_t gg = done + g - 32;
+                if (a.wlog && lane == 0 && tile == G / 2 && gg >= 0 && gg < 64) {
+                    uint64_t* tl = a.wlog + 262144 + ((int64_t)wv * 64 + gg) * 8;
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) tl[j] = ts[j];
+                    tl[5] = (uint64_t)(uint32_t)gmax;
+                }
+#endif
             }
             __builtin_amdgcn_s_setprio(0);
             if (publish) {
