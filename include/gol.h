@@ -197,6 +197,15 @@ gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff);
 gol_status gol_plan_skew(gol_engine* e, uint32_t* rows_old, uint32_t* rows_young,
                          uint32_t* units_old);
 
+/* Column layout of full-depth launches: *strips wavefront strips per row block
+ * and the packed half strip's units (64-lane strips of a one-segment launch: the
+ * last strip ends at the field's right edge and the gap of <= 30 lane groups
+ * before it runs 32 lanes wide, two row blocks per wavefront): *half_units
+ * wavefronts over *half_groups lane groups (both 0 without one).  A resident or
+ * composite engine reports its first stripe / 0.  Out pointers may be NULL. */
+gol_status gol_plan_columns(gol_engine* e, uint32_t* strips, uint32_t* half_units,
+                            uint32_t* half_groups);
+
 /* Resident plan (gol_config.resident): *on = 1 if gol_step runs the resident
  * kernel; then *bands x *strips tiles, one workgroup each (bands, strips may be
  * NULL).  A composite engine reports 0. */

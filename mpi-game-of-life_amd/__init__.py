@@ -34,7 +34,7 @@ EXPORTS = [
     "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
     "gol_create_rank", "gol_create_group", "gol_group_step", "gol_plan_info",
     "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
-    "gol_plan_resident", "gol_plan_skew",
+    "gol_plan_resident", "gol_plan_skew", "gol_plan_columns",
 ]
 
 
@@ -151,6 +151,7 @@ def lib():
     L.gol_plan_handoff.argtypes = [vp, ctypes.POINTER(u32)]
     L.gol_plan_resident.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.gol_plan_skew.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    L.gol_plan_columns.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.gol_create_rank_transport.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32,
                                             ctypes.POINTER(Transport), ctypes.POINTER(vp)]
     L.gol_round_schedule.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32, u64, i32,
@@ -161,7 +162,7 @@ def lib():
                  "gol_sync", "gol_digest", "gol_set_timing", "gol_get_timing",
                  "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
                  "gol_create_group", "gol_group_step", "gol_plan_info", "gol_plan_handoff",
-                 "gol_plan_resident", "gol_plan_skew",
+                 "gol_plan_resident", "gol_plan_skew", "gol_plan_columns",
                  "gol_create_rank_transport", "gol_round_schedule"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
@@ -279,6 +280,10 @@ class Engine:
         _check(lib().gol_plan_skew(self._h, ctypes.byref(ro), ctypes.byref(ry), ctypes.byref(uo)))
         # age-skewed row blocks: (rows_old, rows_young, units_old), or None
         self.age_skew = (ro.value, ry.value, uo.value) if ro.value else None
+        st, hu, hg = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().gol_plan_columns(self._h, ctypes.byref(st), ctypes.byref(hu), ctypes.byref(hg)))
+        # (strips per row block, half-strip units, half-strip lane groups)
+        self.columns = (st.value, hu.value, hg.value)
 
     def close(self):
         if self._h:

@@ -234,6 +234,13 @@ struct gol_engine {
         // first-dispatched units rows_old rows, the others rows_young (both = rpw
         // mod the prefetch block, so the hand-off tail offset is rpw's)
         int32_t rows_old = 0, rows_young = 0, units_old = 0;
+        // 64-lane strips: edge-aligned columns (col_layout) and the packed half
+        // strip's units after the full strips' (pairs: 3 words per unit)
+        int32_t edge = 0;
+        int64_t right_q0 = -1, half_q0 = 0, half_hi = -1;
+        int64_t pair_units = 0, half_rows = 0;
+        std::vector<int64_t> pairs;
+        int64_t* dpairs = nullptr;
         SegDesc* dev = nullptr;
     };
     std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: see RankGeom
@@ -301,13 +308,93 @@ void finish_segs(std::vector<SegDesc>& segs, int64_t rpw, int32_t strips)
     }
 }
 
-// Strip groups per row block for strips of 64 >> shift lanes.
-int32_t strip_groups(uint64_t wq, int shift)
+// 64-lane strips are edge-aligned (StepArgs::edge).  A lane whose neighbour lane
+// is the DPP shift's zero (lane 0 / 63) or lies outside the field sees the dead
+// border, so it is exact without a halo lane: strip 0 outputs groups 0..62, strip
+// s >= 1 groups 62 s + 1 .. 62 s + 62 (lane 0 its halo), and a strip whose lane 63
+// holds group ng - 1 outputs that too.  A row of ng groups takes 1 + ceil((ng -
+// 64) / 62) strips (4096 columns: 1; with a halo lane at both ends: 2).  With the
+// packed half strip (one-segment plans) the last strip is right-aligned (lane 63 =
+// group ng - 1) and the gap of <= 30 groups between it and the strips before it is
+// a 32-lane half strip whose units run two row blocks each: a 65536-column row
+// costs 16.5 wavefronts per row block instead of 17 (262144 columns: 66.5, not 67).
+struct ColLayout {
+    int32_t strips = 0;
+    int64_t right_q0 = -1, half_q0 = 0, half_hi = -1;
+    bool half() const { return half_hi > half_q0; }
+};
+
+ColLayout col_layout(int64_t ng, bool allow_half)
 {
+    ColLayout c;
+    c.strips = 1;
+    if (ng <= 64) return c;
+    const int64_t s0 = 1 + (ng - 64 + 61) / 62;
+    const int64_t S = s0 - 1, gap = ng - 126 - 62 * (S - 2);
+    c.strips = (int32_t)s0;
+    if (allow_half && S >= 2 && gap >= 1 && gap <= 30) {
+        c.strips = (int32_t)S;
+        c.right_q0 = ng - 64;
+        c.half_q0 = 62 * (S - 1);
+        c.half_hi = c.half_q0 + gap;
+    }
+    return c;
+}
+
+// Strip groups per row block for strips of 64 >> shift lanes (shift 0: edge-aligned,
+// with the packed half strip if `half`).
+int32_t strip_groups(uint64_t wq, int shift, bool half = false)
+{
+    if (shift == 0) return col_layout((int64_t)wq, half).strips;
     const uint64_t out = (uint64_t)((64 >> shift) - 2);
     const uint64_t strips = (wq + out - 1) / out;
     const uint64_t per = 1ull << shift;
     return (int32_t)((strips + per - 1) / per);
+}
+
+// Rows per block of the half strip's units (classic closure) for a plan whose
+// blocks have R rows: as long as the plan's blocks by the cost models below
+// (classic R + K + 4; hand-off 1.02 R + 10).
+int64_t half_rows_for(int64_t R, bool hand, int K)
+{
+    if (!hand) return R;
+    return std::max<int64_t>(1, (int64_t)(1.02 * (double)R + 10.0) - K - 4);
+}
+
+// The packed half strip's units of a one-segment plan.  Its column is cut into row
+// blocks of Rp rows from out_lo; two consecutive blocks share a wavefront (lanes
+// 0-31 / 32-63) when they have the same length, every row they stream (with the
+// prefetch overrun) and every row mask they compute lies inside the buffer and the
+// field (the kernel takes the first block's row validity for both), and the second
+// block's row offset fits the 32-bit lane offset.  Other blocks run alone in lanes
+// 0-31.  Returns the unit count; `out` gets (first row A, first row B or -1, rows)
+// per unit.
+int64_t half_units(const SegDesc& sg, int64_t Rp, int K, int planes, int64_t stride,
+                   std::vector<int64_t>* out)
+{
+    if (out) out->clear();
+    const int64_t lo = sg.out_lo, hi = sg.out_hi;
+    if (hi <= lo) return 0;
+    Rp = std::max<int64_t>(1, Rp);
+    const int64_t pf = gol::prefetch_of(K, planes);
+    auto interior = [&](int64_t rb, int64_t re) {
+        return rb - K >= 0 && sg.glob0 + rb >= 2 * (int64_t)K && re + K + pf <= sg.in_rows &&
+               sg.glob0 + re + K + 2 * pf <= sg.field_h;
+    };
+    int64_t units = 0;
+    for (int64_t rb = lo; rb < hi; ++units) {
+        const int64_t la = std::min(Rp, hi - rb), rb2 = rb + la;
+        const int64_t lb = std::min(Rp, hi - rb2);
+        const bool pair = rb2 < hi && la == lb && interior(rb, rb2) && interior(rb2, rb2 + lb) &&
+                          (la + 1) * stride * 8 < (int64_t(1) << 31);
+        if (out) {
+            out->push_back(rb);
+            out->push_back(pair ? rb2 : -1);
+            out->push_back(la);
+        }
+        rb = pair ? rb2 + lb : rb2;
+    }
+    return units;
 }
 
 // Hand-off constraint on the rows per wavefront R of a launch of depth d
@@ -341,11 +428,13 @@ struct RowPlan {
 
 RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K, int planes,
                            int occ_classic, int occ_hand, int simds, int force_rpw,
-                           int force_shift, uint32_t handoff)
+                           int force_shift, uint32_t handoff, int64_t half_stride = 0)
 {
     const int64_t c0 = 3;  // per-wavefront fixed cost, in rows
     int64_t maxrows = 1;
     for (const auto& s : segs) maxrows = std::max<int64_t>(maxrows, s.out_hi - s.out_lo);
+    // the packed half strip (half_stride = the buffer's row stride; 0 = off)
+    const bool half = half_stride > 0 && segs.size() == 1 && col_layout((int64_t)wq, true).half();
     // best [hand][filled]: filled = at least `occ` wavefronts per SIMD
     RowPlan best_p[2][2];
     double best[2][2] = {{1e300, 1e300}, {1e300, 1e300}};
@@ -355,7 +444,8 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
         const int occ = std::max(1, hand ? occ_hand : occ_classic);
         for (int shift = 0; shift <= 2; ++shift) {
             if (force_shift >= 0 && shift != force_shift) continue;
-            const int32_t groups = strip_groups(wq, shift);
+            const bool hs = half && shift == 0;
+            const int32_t groups = strip_groups(wq, shift, hs);
             const int64_t r_lo = force_rpw ? force_rpw : std::max<int64_t>(8, K + 2);
             const int64_t r_hi =
                 force_rpw ? force_rpw : std::max<int64_t>(r_lo, std::min<int64_t>(1024, maxrows + K));
@@ -365,6 +455,9 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
                 for (const auto& sg : segs) {
                     const int64_t nb = (std::max<int64_t>(0, sg.out_hi - sg.out_lo) + R - 1) / R;
                     units += groups * nb;
+                    if (hs)
+                        units += half_units(sg, half_rows_for(R, hand != 0, K), K, planes, half_stride,
+                                            nullptr);
                     blocks_max = std::max(blocks_max, nb);
                 }
                 if (hand && blocks_max < 2) continue;  // nothing to hand over
@@ -411,6 +504,9 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
 constexpr double kAgeRateHand = 0.78, kAgeRateClassic = 0.72;
 
 constexpr double kHandSkewCost = 1.05;
+// Young block length from which skewed classic blocks with the packed half strip
+// are preferred to hand-off blocks (build_plans).
+constexpr int64_t kHalfMinRows = 72;
 
 struct Skew {
     int64_t rows_old = 0, rows_young = 0, nblk = 0;  // rows_old 0 = no skew
@@ -418,7 +514,7 @@ struct Skew {
 };
 
 Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, int occ, int K,
-              int planes, bool hand, int64_t max_units = INT64_MAX)
+              int planes, bool hand, int64_t max_units = INT64_MAX, int64_t half_stride = 0)
 {
     Skew best_s;
     double rho = hand ? kAgeRateHand : kAgeRateClassic;
@@ -428,10 +524,16 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
     const int pf = gol::prefetch_of(K, planes);
     auto cost = [&](int64_t r) { return hand ? 1.02 * (double)r + 10.0 : (double)(r + K + 4); };
     auto fits = [&](int64_t r) { return r >= std::max(8, K + 2) && (!hand || handoff_fits(r, K, planes)); };
+    // the packed half strip's units (half_stride > 0) come after the full strips':
+    // young waves, with blocks as long as the young blocks
+    auto half_n = [&](int64_t ry) {
+        return half_stride > 0 ? half_units(sg, half_rows_for(ry, hand, K), K, planes, half_stride, nullptr)
+                               : (int64_t)0;
+    };
     // the planned equal blocks: nw wavefronts per SIMD run as pairs (old rate 1,
     // young rho) with refills, and the last pair's young wave ends alone
     const int64_t nb0 = (rows + R - 1) / R;
-    const double nw = std::ceil((double)(nb0 * strips) / (double)units_old);
+    const double nw = std::ceil((double)(nb0 * strips + half_n(R)) / (double)units_old);
     double best = std::max(0.0, nw - 2) * cost(R) / (1 + rho) + cost(R) / rho;
     // Lengths step: hand-off blocks keep both lengths in one class mod the
     // prefetch block (one tail offset per launch: R or R + pf/2), classic ones
@@ -475,7 +577,8 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
             }
             if (!ok) continue;
             const double t = std::max(cost(ro), cost(ry) / rho);
-            if (t < best * 0.995) {
+            if (t < best * 0.995 &&
+                (half_stride <= 0 || units + half_n(ry) <= std::min(2 * units_old, max_units))) {
                 best = t;
                 best_s = {ro, ry, nblk, t};
             }
@@ -513,15 +616,18 @@ bool single_stream_skews(uint64_t h, uint64_t w, const gol_config* cfg)
     const int occ_h = hand_ok ? gol::life_blocks_per_cu(K, rule, planes, true) : 0;
     SegDesc s{};
     s.in_rows = s.field_h = s.out_hi = (int64_t)h;
+    const char* dev_pairs = std::getenv("GOL_DEV_PAIRS");
+    const int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) ? 0 : (int64_t)(ng * G);
     for (int hand = 0; hand <= 1; ++hand) {
         if ((hand && (cfg->handoff == 1 || !hand_ok)) || (!hand && cfg->handoff == 2)) continue;
         const RowPlan rp = pick_rows_per_wave({s}, ng, K, planes, occ_c, occ_h, 4 * cus, 0, shift,
-                                              hand ? 2u : 1u);
+                                              hand ? 2u : 1u, hs);
         if (rp.hand != (hand != 0)) continue;
         std::vector<SegDesc> segs{s};
         finish_segs(segs, rp.rpw, rp.groups);
         if (age_skew(segs[0], rp.rpw, rp.groups, (int64_t)gol::kWavesPerBlock * cus,
-                     hand ? occ_h : occ_c, K, planes, hand != 0)
+                     hand ? occ_h : occ_c, K, planes, hand != 0, INT64_MAX,
+                     rp.lane_shift == 0 ? hs : 0)
                 .rows_old)
             return true;
     }
@@ -538,6 +644,18 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                           : 0;
     int64_t max_units = 0;
     bool any_hand = false;
+    // the packed half strip of one-segment plans (col_layout; GOL_DEV_PAIRS=0 turns
+    // it off for A/B): the planners count its units
+    const char* dev_pairs = std::getenv("GOL_DEV_PAIRS");
+    int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) ? 0 : (int64_t)e->stride;
+    auto units_of = [&](const std::vector<SegDesc>& segs, int32_t groups, int shift, int64_t R,
+                        bool hand) {
+        int64_t u = plan_units(segs, groups);
+        if (hs && shift == 0 && segs.size() == 1 && col_layout((int64_t)e->ng, true).half())
+            u += half_units(segs[0], half_rows_for(R, hand, (int)e->K), (int)e->K, e->planes, hs,
+                            nullptr);
+        return u;
+    };
     // hand-off or classic blocks for the whole engine, decided on its widest plan
     // (all launches of a step then share one kernel kind; a plan where hand-off
     // does not fit still falls back to classic blocks)
@@ -545,7 +663,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     if (!gol::handoff_kernel_exists((int)e->K, e->rule)) handoff = 1;
     if (handoff == 0 && !raw.empty())
         handoff = pick_rows_per_wave(raw[0], e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
-                                     (int)e->rows_per_wave, e->lane_shift, 0)
+                                     (int)e->rows_per_wave, e->lane_shift, 0, hs)
                           .hand
                       ? 2
                       : 1;
@@ -554,22 +672,35 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     // modelled row a skewed hand-off launch ran ~5% slower than a skewed classic one
     // at the per-GPU shapes 8448..33024 x 65536 (profiles/r02/ab_skew.jsonl), which
     // puts the crossover between 16640 rows (hand-off) and 33024 (classic).  When
-    // both kinds skew, the modelled times decide.
+    // both kinds skew, the modelled times decide -- except that classic blocks with
+    // the packed half strip win wherever their young blocks reach kHalfMinRows
+    // (profiles/r03/ab_half_strip_handoff.jsonl, TCUPS, hand-off vs classic + half
+    // strip: 8448 rows 111.9 vs 105.2 (young blocks 54 rows), 12288: 118.1 vs 119.1
+    // (80), 16640: 119.8 vs 124.4 (109)), which the row-cost models do not resolve.
     if (e->handoff == 0 && handoff == 2 && raw.size() >= 1 && raw[0].size() == 1 &&
         !e->rows_per_wave && !e->shared_device) {
         const int64_t first = (int64_t)gol::kWavesPerBlock * cus;
         Skew sk[2];
         for (int hand = 0; hand <= 1; ++hand) {
+            const int64_t h_s = hand ? 0 : hs;
             const RowPlan rp = pick_rows_per_wave(raw[0], e->ng, (int)e->K, e->planes, occ_c, occ_h,
-                                                  4 * cus, 0, e->lane_shift, hand ? 2u : 1u);
+                                                  4 * cus, 0, e->lane_shift, hand ? 2u : 1u, h_s);
             if (rp.hand != (hand != 0)) break;
             std::vector<SegDesc> segs = raw[0];
             finish_segs(segs, rp.rpw, rp.groups);
             sk[hand] = age_skew(segs[0], rp.rpw, rp.groups, first, hand ? occ_h : occ_c, (int)e->K,
-                                e->planes, hand != 0);
+                                e->planes, hand != 0, INT64_MAX, rp.lane_shift == 0 ? h_s : 0);
         }
-        if (sk[0].rows_old && (!sk[1].rows_old || sk[0].t < sk[1].t * kHandSkewCost)) handoff = 1;
+        if (sk[0].rows_old && hs && col_layout((int64_t)e->ng, true).half() &&
+            sk[0].rows_young >= kHalfMinRows)
+            handoff = 1;
+        else if (sk[0].rows_old && (!sk[1].rows_old || sk[0].t < sk[1].t * kHandSkewCost))
+            handoff = 1;
     }
+    // Hand-off plans run without the half strip: its units close their blocks the
+    // classic way, and beside short hand-off blocks that lost (8448 rows 111.9 ->
+    // 109.4, 8416 111.6 -> 104.0 TCUPS; +1% at 12288 and 16640).
+    if (handoff == 2) hs = 0;
     for (size_t pi = 0; pi < raw.size(); ++pi) {
         const auto& r = raw[pi];
         gol_engine::Plan p;
@@ -580,7 +711,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         const bool inner = e->overlap && pi == (size_t)e->Hx + 1;
         const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
                                               (int)e->rows_per_wave, e->lane_shift,
-                                              band ? 1u : handoff);
+                                              band ? 1u : handoff, hs);
         p.rpw = rp.rpw;
         p.groups = rp.groups;
         p.lane_shift = rp.lane_shift;
@@ -601,7 +732,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
             p.hand = false;
         }
         finish_segs(p.segs, p.rpw, p.groups);
-        p.total_units = plan_units(p.segs, p.groups);
+        p.total_units = units_of(p.segs, p.groups, p.lane_shift, p.rpw, p.hand);
         int64_t cap = INT64_MAX;
         if (inner && !e->rows_per_wave && !e->shared_device) {
             const int occ = p.hand ? occ_h : occ_c;
@@ -613,28 +744,28 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                     ++R;
                     if (p.hand && !handoff_fits(R, (int)e->K, e->planes)) continue;
                     finish_segs(segs, R, p.groups);
-                } while (plan_units(segs, p.groups) > cap && R < 4096);
+                } while (units_of(segs, p.groups, p.lane_shift, R, p.hand) > cap && R < 4096);
                 p.rpw = R;
                 p.segs = segs;
-                p.total_units = plan_units(p.segs, p.groups);
+                p.total_units = units_of(p.segs, p.groups, p.lane_shift, p.rpw, p.hand);
             }
         }
         if (!band && p.segs.size() == 1 && !e->rows_per_wave && !e->shared_device) {
             const int occ = p.hand ? occ_h : occ_c;
             const int64_t first = slots_first;
             Skew sk = age_skew(p.segs[0], p.rpw, p.groups, first, occ, (int)e->K, e->planes,
-                               p.hand, cap);
+                               p.hand, cap, p.lane_shift == 0 ? hs : 0);
             // Auto block kind, per plan: hand-off lengths are confined to two classes
             // mod the prefetch block, which can leave a launch without a close
             // one-round fit (8416 rows in 113 blocks of 86/62 rows: 90 vs 77 us); a
             // skewed classic plan is taken when the model says it is faster.
             if (p.hand && e->handoff == 0) {
                 const RowPlan rc = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h,
-                                                      4 * cus, 0, e->lane_shift, 1u);
+                                                      4 * cus, 0, e->lane_shift, 1u, hs);
                 std::vector<SegDesc> cs = r;
                 finish_segs(cs, rc.rpw, rc.groups);
                 const Skew skc = age_skew(cs[0], rc.rpw, rc.groups, first, occ_c, (int)e->K,
-                                          e->planes, false, cap);
+                                          e->planes, false, cap, rc.lane_shift == 0 ? hs : 0);
                 if (!rc.hand && skc.rows_old &&
                     (!sk.rows_old || skc.t < sk.t * kHandSkewCost)) {
                     p.hand = false;
@@ -653,6 +784,30 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                 p.total_units = plan_units(p.segs, p.groups);
                 // the launch's hand-off tail offset follows the lengths' class
                 p.rpw = sk.rows_young;
+            }
+        }
+        // 64-lane strips: edge-aligned columns; one-segment plans also pack the
+        // half strip into units after the full strips' (young waves, blocks as long
+        // as the young ones)
+        if (p.lane_shift == 0) {
+            const ColLayout cl = col_layout((int64_t)e->ng, hs && p.segs.size() == 1);
+            p.edge = 1;
+            if (p.groups != cl.strips) {  // a planner's fallback plan: equal blocks
+                p.groups = cl.strips;
+                p.rows_old = p.rows_young = p.units_old = 0;
+                finish_segs(p.segs, p.rpw, p.groups);
+            }
+            p.total_units = plan_units(p.segs, p.groups);
+            if (cl.half()) {
+                p.right_q0 = cl.right_q0;
+                p.half_q0 = cl.half_q0;
+                p.half_hi = cl.half_hi;
+                p.half_rows = half_rows_for(p.rpw, p.hand, (int)e->K);
+                p.pair_units = half_units(p.segs[0], p.half_rows, (int)e->K, e->planes, hs, &p.pairs);
+                p.total_units += p.pair_units;
+                HIP_TRY(hipMalloc(&p.dpairs, sizeof(int64_t) * p.pairs.size()));
+                HIP_TRY(hipMemcpy(p.dpairs, p.pairs.data(), sizeof(int64_t) * p.pairs.size(),
+                                  hipMemcpyHostToDevice));
             }
         }
         for (const auto& sg : p.segs) {
@@ -677,11 +832,20 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         any_hand |= p.hand && p.multi_blk;
         if (std::getenv("GOL_DEV_PLANS"))  // dev: the launch plans as built
             std::fprintf(stderr, "plan %zu: rows [%lld, %lld) x %zu segs, R %lld, strips %d, units %lld, "
-                         "hand %d, skew %d/%d\n", pi, (long long)p.segs[0].out_lo,
-                         (long long)p.segs[0].out_hi, p.segs.size(), (long long)p.rpw, p.groups,
-                         (long long)p.total_units, (int)p.hand, p.rows_old, p.rows_young);
-        HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * p.segs.size()));
-        HIP_TRY(hipMemcpy(p.dev, p.segs.data(), sizeof(SegDesc) * p.segs.size(),
+                         "hand %d, skew %d/%d, half-strip units %lld (rows %lld)\n", pi,
+                         (long long)p.segs[0].out_lo, (long long)p.segs[0].out_hi, p.segs.size(),
+                         (long long)p.rpw, p.groups, (long long)p.total_units, (int)p.hand,
+                         p.rows_old, p.rows_young, (long long)p.pair_units, (long long)p.half_rows);
+        // device segment table: + the half strip's one-block segment (StepArgs::pairs)
+        std::vector<SegDesc> dsegs = p.segs;
+        if (p.pair_units) {
+            SegDesc hs_seg = p.segs[0];
+            hs_seg.nblk = 1;
+            hs_seg.unit0 = p.total_units - p.pair_units;
+            dsegs.push_back(hs_seg);
+        }
+        HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * dsegs.size()));
+        HIP_TRY(hipMemcpy(p.dev, dsegs.data(), sizeof(SegDesc) * dsegs.size(),
                           hipMemcpyHostToDevice));
         e->plans.push_back(p);
     }
@@ -1250,7 +1414,7 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     a.in = e->buf[e->cur];
     a.out = e->buf[e->cur ^ 1];
     a.segs = p.dev;
-    a.nseg = (int32_t)p.segs.size();
+    a.nseg = (int32_t)p.segs.size() + (p.pair_units ? 1 : 0);
     a.strips = p.groups;
     a.lane_shift = p.lane_shift;
     a.stride = (int64_t)e->stride;
@@ -1276,6 +1440,13 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         a.rows_old = p.rows_old;
         a.units_old = p.units_old;
     }
+    a.edge = p.edge;
+    a.right_q0 = p.right_q0;
+    a.half_q0 = p.half_q0;
+    a.half_hi = p.half_hi;
+    a.pair_units = p.pair_units;
+    a.pair0 = p.total_units - p.pair_units;
+    a.pairs = p.dpairs;
 #if GOL_EXP
     a.wlog = g_dev_wave_log;
     a.prog = g_dev_prog;
@@ -1294,8 +1465,13 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
             const double classic = hand ? (double)std::min<int64_t>(1, sg.nblk) : (double)sg.nblk;
             comp += depth * n + classic * depth * (depth - 1.0);
         }
-        const double cols = (double)p.groups * 64.0 * 32.0 * e->planes;
-        GOL_TRY(timing_end(e, s, e0, e1, p.own_rows * (double)e->W * depth, comp * cols));
+        // (the half strip's units: 64 lanes over one block's rows each, classic)
+        double comp_half = 0;
+        for (size_t i = 0; i + 2 < p.pairs.size(); i += 3)
+            comp_half += depth * (double)p.pairs[i + 2] + depth * (depth - 1.0);
+        const double cols = 64.0 * 32.0 * e->planes;  // per strip or unit
+        GOL_TRY(timing_end(e, s, e0, e1, p.own_rows * (double)e->W * depth,
+                           (comp * p.groups + comp_half) * cols));
     }
     if (swap) e->cur ^= 1;
     return GOL_OK;
@@ -1756,8 +1932,10 @@ void gol_destroy(gol_engine* e)
         if (ev) (void)hipEventDestroy(ev);
     if (e->band_stream) (void)hipStreamDestroy(e->band_stream);
     if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
-    for (auto& p : e->plans)
+    for (auto& p : e->plans) {
         if (p.dev) (void)hipFree(p.dev);
+        if (p.dpairs) (void)hipFree(p.dpairs);
+    }
     for (int b = 0; b < 2; ++b) {
         if (e->alloc[b]) (void)hipFree(e->alloc[b]);
         if (e->side[b]) (void)hipFree(e->side[b]);
@@ -2398,6 +2576,21 @@ gol_status gol_plan_skew(gol_engine* e, uint32_t* rows_old, uint32_t* rows_young
     if (units_old) *units_old = on ? (uint32_t)p.units_old : 0u;
     return GOL_OK;
 }
+gol_status gol_plan_columns(gol_engine* e, uint32_t* strips, uint32_t* half_units,
+                            uint32_t* half_groups)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) return gol_plan_columns(e->parts[0], strips, half_units, half_groups);
+    if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
+    const auto& p = e->nranks > 1 ? e->plans[e->Hx - 1] : e->plans[0];
+    const bool on = !e->res.on;
+    if (strips) *strips = on ? (uint32_t)p.groups : (uint32_t)e->res.strips;
+    if (half_units) *half_units = on ? (uint32_t)p.pair_units : 0u;
+    if (half_groups)
+        *half_groups = on && p.pair_units ? (uint32_t)(p.half_hi - p.half_q0) : 0u;
+    return GOL_OK;
+}
+
 gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint32_t* strips)
 {
     if (!e || !on) return fail(GOL_EINVAL, "null argument");

@@ -76,6 +76,23 @@ struct StepArgs {
     int64_t side_slot;    // words per slot: 2 (K-1) rows x 64 lanes x NP/2 words
     uint64_t* wlog;       // dev timing builds only (GOL_EXP & 128): 4 words per wavefront
     uint32_t* prog;       // dev (GOL_EXP & 1024): per-SIMD wave progress, 2 words per SIMD
+    // Edge-aligned strips and the packed half strip (engine.cpp col_layout;
+    // one-segment launches of 64-lane strips).  A lane whose neighbour lane is the
+    // DPP shift's zero (lane 0 / 63) or outside the field is exact, so strip 0 starts
+    // at group 0 (63 output groups), strip s at group 62 s (lane 0 its halo), and
+    // the last strip ends at group ng - 1 in lane 63 (right_q0 = ng - 64; -1: 62 s).
+    // The gap of <= 30 groups left between the last two strips is the half strip
+    // [half_q0 + 1, half_hi]: 32 lanes.  Units [pair0, pair0 + pair_units) run it,
+    // two row blocks per wavefront (lanes 32-63 offset by the second block's rows),
+    // with classic block closure (the device segment table carries one more
+    // segment for them: a copy of segment 0 with nblk = 1 and unit0 = pair0, so
+    // that no unit of theirs is a hand-off producer or consumer); pairs holds
+    // (first row A, first row B or -1 for lanes 32-63 idle, rows) per unit.
+    int32_t edge;
+    int64_t right_q0;
+    int64_t half_q0, half_hi;
+    int64_t pair0, pair_units;
+    const int64_t* pairs;
 };
 
 // Fused depths with an instantiated kernel, largest first.  The shipped library

@@ -16,7 +16,11 @@
 //     with the carry bit from the adjacent lane by a DPP wave shift.  After g
 //     fused generations the contamination from the unknown groups beyond the
 //     halo lanes has moved g columns into lanes 0/63, so K <= 63 keeps lanes
-//     1..62 exact.
+//     1..62 exact.  64-lane strips are edge-aligned (StepArgs::edge): a lane
+//     next to the DPP shift's zero (lane 0 / 63) or to a lane outside the field
+//     sees the dead border, so strip 0 starts at group 0 and the last strip of a
+//     one-segment launch ends at group ng - 1; the gap of <= 30 groups before it
+//     is a 32-lane "half strip" whose wavefronts carry two row blocks.
 //   * The wavefront streams down the rows of its row block.  Generation g
 //     (stage g-1, g = 1..K) keeps a 3-row window in registers: for each incoming
 //     row it forms the horizontal 3-cell sum H3 (bit-sliced sum + carry) once and
@@ -368,39 +372,75 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
         if (unit >= a.segs[j].unit0) sidx = j;
     const SegDesc sg = a.segs[sidx];
     const int64_t u = unit - sg.unit0;
+    // a unit of the packed half strip (uniform): its two row blocks from the table
+    const bool pu = a.pair_units > 0 && unit >= a.pair0;
+    int64_t pair_a = 0, pair_b = -1, pair_len = 0;
+    if (pu) {
+        // (row indices < 2^31; readfirstlane keeps them, and every row bound derived
+        // from them, in SGPRs)
+        const int64_t* pd = a.pairs + 3 * (unit - a.pair0);
+        pair_a = __builtin_amdgcn_readfirstlane((int32_t)pd[0]);
+        pair_b = __builtin_amdgcn_readfirstlane((int32_t)pd[1]);
+        pair_len = __builtin_amdgcn_readfirstlane((int32_t)pd[2]);
+    }
     // row blocks bottom-up: the block below (a hand-off producer) has the smaller index
-    const int64_t blk = sg.nblk - 1 - u / a.strips;
+    const int64_t blk = pu ? 0 : sg.nblk - 1 - u / a.strips;
     // strip `strip` of the row block lives in lanes [sub*L, sub*L + L); the DPP
     // shifts cross from one strip into the next only at halo lanes
     const int lshift = a.lane_shift;
     const int L = 64 >> lshift;
     const int sub = lane >> (6 - lshift);
     const int lin = lane & (L - 1);
-    // lane group of this lane: q = qbase + sub*(L-2) + lin, qbase (uniform) the
-    // group one left of the wave's first strip; its column mask (columns >= w dead)
-    const int64_t qbase = (u % a.strips) * (int64_t)(1 << lshift) * (L - 2) - 1;
-    const int64_t q = qbase + sub * (L - 2) + lin;
-    const bool qin = (q >= 0) && (q < a.ng);
+    // lane group q of this lane, the group `qfirst` in the strip's first lane, and
+    // whether the lane's result is exact (an output lane)
+    int64_t q, qfirst;
+    bool exact, on = true;
+    if (pu) {
+        // half strip: lanes 0 and 31 of each half are its halo
+        const int hl = lane & 31;
+        qfirst = a.half_q0;
+        q = qfirst + hl;
+        exact = hl >= 1 && q <= a.half_hi;
+        on = lane < 32 || pair_b >= 0;
+    } else if (a.edge) {
+        const int64_t s = u % a.strips;
+        qfirst = s == 0 ? 0 : (s == a.strips - 1 && a.right_q0 >= 0) ? a.right_q0 : 62 * s;
+        q = qfirst + lane;
+        exact = (lane >= 1 || q == 0) && (lane <= 62 || q == a.ng - 1);
+    } else {
+        // q = qbase + sub*(L-2) + lin, qbase (uniform) the group one left of the
+        // wave's first strip
+        const int64_t qbase = (u % a.strips) * (int64_t)(1 << lshift) * (L - 2) - 1;
+        qfirst = qbase + 1;
+        q = qbase + sub * (L - 2) + lin;
+        exact = lin >= 1 && lin <= L - 2;
+    }
+    const bool qin = on && (q >= 0) && (q < a.ng);
+    // column mask (columns >= w dead)
     Pl<NP> cm;
 #pragma unroll
     for (int k = 0; k < NP; ++k)
         cm.v[k] = qin ? ((q == a.ng - 1) ? (uint32_t)(a.lastmask[k / 2] >> (32 * (k & 1))) : ~0u)
                       : 0u;
-    // lanes outside the field read the strip's first group (any word of the row
-    // will do; masked to 0)
-    const int64_t qc = qin ? q : qbase + 1;
+    // lanes outside the field read a group of the strip (any word of the row will
+    // do; masked to 0)
+    const int64_t qc = qin ? q : min(qfirst + 1, a.ng - 1);
     // Every access = a uniform row base (SGPRs) + a per-lane byte offset: the
-    // lane's group in field rows, the lane itself in side rows (halo lanes and
-    // lanes outside the field share groups with other lanes, so side rows, which
-    // every lane stores, are indexed by lane)
-    const uint32_t voff = (uint32_t)(qc * G * 8);
+    // lane's group in field rows (lanes 32-63 of a pair unit: plus their row
+    // block's offset), the lane itself in side rows (halo lanes and lanes outside
+    // the field share groups with other lanes, so side rows, which every lane
+    // stores, are indexed by lane)
+    const int64_t row_off = (pu && lane >= 32 && pair_b >= 0) ? (pair_b - pair_a) * a.stride : 0;
+    const uint32_t voff = (uint32_t)((qc * G + row_off) * 8);
     const uint32_t voff_side = (uint32_t)(lane * G * 8);
 
     // row block [rb, re): rows_per_wave rows each, or with age-skewed blocks
     // (one segment) the bottom blocks of a strip whose units start first (u <
-    // units_old, the older wave of their SIMD) rows_old rows each
-    int64_t rb = sg.out_lo + blk * a.rows_per_wave, rlen = a.rows_per_wave;
-    if (a.rows_old) {
+    // units_old, the older wave of their SIMD) rows_old rows each; a pair unit's
+    // from the table
+    int64_t rb = pu ? pair_a : sg.out_lo + blk * a.rows_per_wave;
+    int64_t rlen = pu ? pair_len : a.rows_per_wave;
+    if (a.rows_old && !pu) {
         const int64_t s = u % a.strips;
         const int64_t jo = min(sg.nblk, max((int64_t)0, (a.units_old - s + a.strips - 1) / a.strips));
         const int64_t ny = sg.nblk - jo;  // young blocks, on top
@@ -416,6 +456,9 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     const int64_t row_first = rb - K;              // local row of step 0
     // hand-off roles: every block but the top one produces side rows for the block
     // above; every block but the bottom one consumes those of the block below
+    // (pair units close their blocks the classic way: their segment, the last of
+    // the launch, is one block deep.  A pu term here instead costs the hand-off
+    // kernels ~80 VGPRs: the compiler specializes the stream on it.)
     const bool producer = HAND && blk > 0;
     const bool consumer = HAND && blk < sg.nblk - 1;
     // a consumer streams R + 2 input rows (steps < t_side), then side rows
@@ -428,7 +471,7 @@ __global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
     char* my_side = HAND ? reinterpret_cast<char*>(a.side + unit * a.side_slot) : nullptr;
     const char* dn_side =
         HAND ? reinterpret_cast<const char*>(a.side + (unit - a.strips) * a.side_slot) : nullptr;
-    const bool st_lane = qin && lin >= 1 && lin <= L - 2;
+    const bool st_lane = qin && exact;
 
     // field-row validity of the row of step t (dead border) and buffer-row validity:
     // steps [t_lo, t_hi) read rows inside both

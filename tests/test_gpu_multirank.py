@@ -197,12 +197,12 @@ def test_one_waiting_launch_per_device(pkg, oracle):
 
 
 def test_waiting_kernel_registry_two_default_engines(pkg, oracle):
-    """Two default engines of one process on one GPU at a hand-off shape (16640 x
+    """Two default engines of one process on one GPU at a hand-off shape (8448 x
     65536: one-round launches with hand-off blocks when alone), stepped without
     syncs in between: only the first keeps hand-off blocks (engine.cpp wait
     registry), both fields exact; a small field created while it lives runs the
     streaming kernel, and gets the resident kernel again once it is gone."""
-    h, w, gens = 16640, 65536, 48
+    h, w, gens = 8448, 65536, 48
     want = oracle.bp_digest(oracle.bp_run(oracle.bp_random(h, w, 5), w, gens, oracle.CONWAY,
                                           threads=16), w)
     a = pkg.Engine(h, w, rule=pkg.CONWAY, device=0)
