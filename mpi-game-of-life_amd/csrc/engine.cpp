@@ -699,8 +699,9 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     }
     // Hand-off plans run without the half strip: its units close their blocks the
     // classic way, and beside short hand-off blocks that lost (8448 rows 111.9 ->
-    // 109.4, 8416 111.6 -> 104.0 TCUPS; +1% at 12288 and 16640).
-    if (handoff == 2) hs = 0;
+    // 109.4, 8416 111.6 -> 104.0 TCUPS; +1% at 12288 and 16640).  (GOL_DEV_PAIRS=2
+    // keeps it, for A/B.)
+    if (handoff == 2 && !(dev_pairs && std::atoi(dev_pairs) == 2)) hs = 0;
     for (size_t pi = 0; pi < raw.size(); ++pi) {
         const auto& r = raw[pi];
         gol_engine::Plan p;
