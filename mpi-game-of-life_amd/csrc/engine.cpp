@@ -355,10 +355,20 @@ int32_t strip_groups(uint64_t wq, int shift, bool half = false)
 // Rows per block of the half strip's units (classic closure) for a plan whose
 // blocks have R rows: as long as the plan's blocks by the cost models below
 // (classic R + K + 4; hand-off 1.02 R + 10).
+// Under hand-off blocks the half strip's classic blocks get 0.8 of that: the
+// classic cost model undercounts short classic blocks (A/B of the scale, one
+// process: 8448 rows 111.2 without the half strip, 115.5-116.7 with it at 0.7-0.9
+// (109.9 at 1.0); 12288: 117.2 vs 123.5-124.6 (119.5 at 1.0);
+// profiles/r03/ab_half_strip_handoff_scale*.jsonl).  GOL_DEV_HALF_SCALE overrides
+// it (dev A/B).
+constexpr double kHalfHandScale = 0.8;
+
 int64_t half_rows_for(int64_t R, bool hand, int K)
 {
     if (!hand) return R;
-    return std::max<int64_t>(1, (int64_t)(1.02 * (double)R + 10.0) - K - 4);
+    double f = kHalfHandScale;
+    if (const char* v = std::getenv("GOL_DEV_HALF_SCALE")) f = std::atof(v);
+    return std::max<int64_t>(1, (int64_t)(f * (double)((int64_t)(1.02 * (double)R + 10.0) - K - 4)));
 }
 
 // The packed half strip's units of a one-segment plan.  Its column is cut into row
@@ -504,9 +514,9 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
 constexpr double kAgeRateHand = 0.78, kAgeRateClassic = 0.72;
 
 constexpr double kHandSkewCost = 1.05;
-// Young block length from which skewed classic blocks with the packed half strip
-// are preferred to hand-off blocks (build_plans).
-constexpr int64_t kHalfMinRows = 72;
+// Young block length from which skewed classic blocks are preferred to hand-off
+// blocks when both run the packed half strip (build_plans).
+constexpr int64_t kHalfClassicRows = 160;
 
 struct Skew {
     int64_t rows_old = 0, rows_young = 0, nblk = 0;  // rows_old 0 = no skew
@@ -536,8 +546,8 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
     const double nw = std::ceil((double)(nb0 * strips + half_n(R)) / (double)units_old);
     double best = std::max(0.0, nw - 2) * cost(R) / (1 + rho) + cost(R) / rho;
     // Lengths step: hand-off blocks keep both lengths in one class mod the
-    // prefetch block (one tail offset per launch: R or R + pf/2), classic ones
-    // take any length.
+    // prefetch block (one tail offset per launch: R + 2c, the classes whose
+    // offset has a kernel pass `fits`), classic ones take any length.
     const int step = hand ? pf : 1;
     // every block count of one round of more than units_old (= one per SIMD)
     // wavefronts: the old blocks from the mean length to twice it
@@ -552,8 +562,8 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
         // at most ~256 old lengths per block count (long blocks step coarser), so
         // that plan building stays fast for tall fields and many rank plans
         const int64_t stride = step * std::max<int64_t>(1, mean / (256 * step));
-        for (int cls = 0; cls < (hand ? 2 : 1); ++cls)
-        for (int64_t ro = mean + ((R + cls * pf / 2 - mean) % step + step) % step;
+        for (int cls = 0; cls < (hand ? pf / 2 : 1); ++cls)
+        for (int64_t ro = mean + ((R + 2 * cls - mean) % step + step) % step;
              ro <= 2 * mean + pf; ro += stride) {
             // the young length: the least in ro's class mod step that covers every
             // strip
@@ -647,7 +657,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     // the packed half strip of one-segment plans (col_layout; GOL_DEV_PAIRS=0 turns
     // it off for A/B): the planners count its units
     const char* dev_pairs = std::getenv("GOL_DEV_PAIRS");
-    int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) ? 0 : (int64_t)e->stride;
+    const int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) ? 0 : (int64_t)e->stride;
     auto units_of = [&](const std::vector<SegDesc>& segs, int32_t groups, int shift, int64_t R,
                         bool hand) {
         int64_t u = plan_units(segs, groups);
@@ -672,36 +682,32 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     // modelled row a skewed hand-off launch ran ~5% slower than a skewed classic one
     // at the per-GPU shapes 8448..33024 x 65536 (profiles/r02/ab_skew.jsonl), which
     // puts the crossover between 16640 rows (hand-off) and 33024 (classic).  When
-    // both kinds skew, the modelled times decide -- except that classic blocks with
-    // the packed half strip win wherever their young blocks reach kHalfMinRows
-    // (profiles/r03/ab_half_strip_handoff.jsonl, TCUPS, hand-off vs classic + half
-    // strip: 8448 rows 111.9 vs 105.2 (young blocks 54 rows), 12288: 118.1 vs 119.1
-    // (80), 16640: 119.8 vs 124.4 (109)), which the row-cost models do not resolve.
+    // both kinds skew, the modelled times decide -- except where the packed half
+    // strip applies: then classic blocks win once their young blocks reach
+    // kHalfClassicRows (profiles/r03/ab_half_strip_handoff_scale_sweep.jsonl, TCUPS,
+    // hand-off vs classic, both with the half strip: 8448 rows 116.7 vs 104.8, 12288
+    // 124.1 vs 119.0, 16640 124.5-126.7 vs 124.3 (classic young blocks 109 rows),
+    // 33024 128.1 vs 130.4 (220)), which the row-cost models do not resolve.
     if (e->handoff == 0 && handoff == 2 && raw.size() >= 1 && raw[0].size() == 1 &&
         !e->rows_per_wave && !e->shared_device) {
         const int64_t first = (int64_t)gol::kWavesPerBlock * cus;
         Skew sk[2];
         for (int hand = 0; hand <= 1; ++hand) {
-            const int64_t h_s = hand ? 0 : hs;
             const RowPlan rp = pick_rows_per_wave(raw[0], e->ng, (int)e->K, e->planes, occ_c, occ_h,
-                                                  4 * cus, 0, e->lane_shift, hand ? 2u : 1u, h_s);
+                                                  4 * cus, 0, e->lane_shift, hand ? 2u : 1u, hs);
             if (rp.hand != (hand != 0)) break;
             std::vector<SegDesc> segs = raw[0];
             finish_segs(segs, rp.rpw, rp.groups);
             sk[hand] = age_skew(segs[0], rp.rpw, rp.groups, first, hand ? occ_h : occ_c, (int)e->K,
-                                e->planes, hand != 0, INT64_MAX, rp.lane_shift == 0 ? h_s : 0);
+                                e->planes, hand != 0, INT64_MAX, rp.lane_shift == 0 ? hs : 0);
         }
-        if (sk[0].rows_old && hs && col_layout((int64_t)e->ng, true).half() &&
-            sk[0].rows_young >= kHalfMinRows)
+        if (hs && col_layout((int64_t)e->ng, true).half()) {
+            if (sk[0].rows_old && (!sk[1].rows_old || sk[0].rows_young >= kHalfClassicRows))
+                handoff = 1;
+        } else if (sk[0].rows_old && (!sk[1].rows_old || sk[0].t < sk[1].t * kHandSkewCost)) {
             handoff = 1;
-        else if (sk[0].rows_old && (!sk[1].rows_old || sk[0].t < sk[1].t * kHandSkewCost))
-            handoff = 1;
+        }
     }
-    // Hand-off plans run without the half strip: its units close their blocks the
-    // classic way, and beside short hand-off blocks that lost (8448 rows 111.9 ->
-    // 109.4, 8416 111.6 -> 104.0 TCUPS; +1% at 12288 and 16640).  (GOL_DEV_PAIRS=2
-    // keeps it, for A/B.)
-    if (handoff == 2 && !(dev_pairs && std::atoi(dev_pairs) == 2)) hs = 0;
     for (size_t pi = 0; pi < raw.size(); ++pi) {
         const auto& r = raw[pi];
         gol_engine::Plan p;

@@ -123,17 +123,22 @@ constexpr int warm_steps_of(int K, int planes)
 {
     return (2 * K + prefetch_of(K, planes) - 1) / prefetch_of(K, planes) * prefetch_of(K, planes);
 }
-// Hand-off kernels exist for tail offsets 0 and prefetch/2: a consumer block of R
-// rows streams R + 2 input steps after the warm-up, i.e. (R + 2 - warm) mod
-// prefetch must be one of them, and at least two whole steady blocks must precede
-// the tail (the flag wait sits at the end of the first of them).  Returns the
-// offset, or -1 if R does not fit.
+// Tail offsets with a hand-off kernel: 0 and prefetch/2, and 6 with the 8-step
+// prefetch block (offset 2 there needs 258 VGPRs: one wave per SIMD).
+constexpr bool handoff_toff_exists(int off, int pf)
+{
+    return off == 0 || off == pf / 2 || (pf == 8 && off == 6);
+}
+// A consumer block of R rows streams R + 2 input steps after the warm-up, i.e.
+// (R + 2 - warm) mod prefetch must be an offset with a kernel, and at least two
+// whole steady blocks must precede the tail (the flag wait sits at the end of the
+// first of them).  Returns the offset, or -1 if R does not fit.
 constexpr int handoff_toff(int64_t R, int K, int planes)
 {
     const int pf = prefetch_of(K, planes), warm = warm_steps_of(K, planes);
     if (K < kHandoffMinDepth || R + 2 < warm + 2 * pf) return -1;
     const int off = (int)((R + 2 - warm) % pf);
-    if (off != 0 && off != pf / 2) return -1;
+    if (!handoff_toff_exists(off, pf)) return -1;
     return R + 2 - off >= warm + 2 * pf ? off : -1;
 }
 

@@ -814,8 +814,8 @@ int occupancy_kernel(RuleKind rule)
 
 // 2-plane lane groups at every depth; 4-plane ones (dev build) up to depth 16,
 // where 5 planes x 4 x K state words still fit the register file.  Hand-off
-// kernels from kHandoffMinDepth on, with tail offsets 0 and kPrefetch/2
-// (handoff_toff in life_internal.h).
+// kernels from kHandoffMinDepth on, with tail offsets 0, kPrefetch/2 and (8-step
+// prefetch) 6 (handoff_toff in life_internal.h).
 constexpr bool depth_has_planes(int K, int NP) { return NP == 2 || (kDevKernels && NP == 4 && K <= 16); }
 
 template <int K, int NP>
@@ -823,9 +823,12 @@ hipError_t launch_planes(const StepArgs& a, RuleKind rule, bool hand, hipStream_
 {
     if constexpr (K >= kHandoffMinDepth) {
         if (hand) {
-            constexpr int half = kPfOf<NP, K>() / 2;
+            // tail offsets 0, pf/2 and (pf = 8) 6: handoff_toff_exists
+            constexpr int pf = kPfOf<NP, K>();
             if (a.tail_off == 0) return launch_kernel<K, NP, true, 0>(a, rule, s);
-            if (a.tail_off == half) return launch_kernel<K, NP, true, half>(a, rule, s);
+            if (a.tail_off == pf / 2) return launch_kernel<K, NP, true, pf / 2>(a, rule, s);
+            if constexpr (pf == 8)
+                if (a.tail_off == 6) return launch_kernel<K, NP, true, (pf == 8 ? 6 : 0)>(a, rule, s);
             return hipErrorInvalidValue;
         }
     }

@@ -58,7 +58,8 @@ def test_half_strip_vs_oracle(pkg, oracle, w, rule):
 @pytest.mark.parametrize("rule", ["ref", "conway"])
 def test_half_strip_depth16_skewed_vs_oracle(pkg, oracle, rule):
     """A per-GPU stripe shape of the 8-way split with classic blocks (age-skewed)
-    and the half strip, one K = 16 launch."""
+    and the half strip, one K = 16 launch (the hand-off default with it:
+    test_gpu_skew.py)."""
     h, w = 8448, 65536
     R = rule_of(pkg, rule)
     with pkg.Engine(h, w, rule=R, device=0, streams=1, handoff=1) as e:
@@ -88,11 +89,31 @@ def test_half_strip_equals_full_strips(pkg, monkeypatch, h, w):
         assert e.digest() == got
 
 
-@pytest.mark.parametrize("h,hand,half", [(8448, True, False), (16640, False, True),
-                                         (65536, False, True)])
+@pytest.mark.parametrize("h,hand,half", [(8448, True, True), (16640, True, True),
+                                         (33024, False, True), (65536, False, True)])
 def test_block_kind_policy(pkg, h, hand, half):
     """The planner's choice per stripe height (engine.cpp build_plans,
-    kHalfMinRows): hand-off blocks without the half strip for short stripes,
-    classic blocks with it from ~12k rows on (profiles/r03/ab_half_strip*.jsonl)."""
+    kHalfClassicRows): hand-off blocks for short stripes, classic blocks once their
+    young blocks reach 160 rows, both with the half strip
+    (profiles/r03/ab_half_strip_handoff_scale_sweep.jsonl)."""
     with pkg.Engine(h, 65536, device=0, streams=1) as e:
         assert e.handoff == hand and (e.columns[1] > 0) == half, (e.handoff, e.columns)
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+@pytest.mark.parametrize("R,toff", [(62, 0), (66, 4), (68, 6)])
+def test_handoff_tail_offsets_vs_oracle(pkg, oracle, R, toff, rule):
+    """Hand-off blocks of every tail offset with a kernel at depth 16 (0, 4 and,
+    r03, 6: (R + 2 - 32) mod 8), with the half strip (8192 columns: a 2-group
+    gap), two launches and a remainder, against the oracle."""
+    assert (R + 2 - 32) % 8 == toff
+    h, w, gens, seed = 900, 8192, 2 * 16 + 5, 13
+    Rr = rule_of(pkg, rule)
+    with pkg.Engine(h, w, rule=Rr, device=0, tb_depth=16, rows_per_wave=R, handoff=2,
+                    streams=1, resident=1) as e:
+        assert e.handoff and e.columns[1] > 0, (e.handoff, e.columns)
+        e.init_random(seed)
+        e.step(gens)
+        got = e.digest()
+    g = oracle.bp_run(oracle.bp_random(h, w, seed), w, gens, Rr, threads=THREADS)
+    assert got == oracle.bp_digest(g, w)
