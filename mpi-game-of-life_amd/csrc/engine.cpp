@@ -409,7 +409,7 @@ int64_t half_units(const SegDesc& sg, int64_t Rp, int K, int planes, int64_t str
 
 // Hand-off constraint on the rows per wavefront R of a launch of depth d
 // (gol::handoff_toff): a consumer block streams R + 2 input rows, kernels exist
-// for two alignments of that count to the prefetch blocks, and the refill that
+// for two or three alignments of that count to the prefetch blocks, and the refill that
 // first fetches side rows (the flag wait sits in front of it) must come after the
 // unrolled warm-up blocks.
 bool handoff_fits(int64_t R, int d, int planes) { return gol::handoff_toff(R, d, planes) >= 0; }
