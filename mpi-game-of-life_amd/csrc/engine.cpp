@@ -259,6 +259,7 @@ struct gol_engine {
         int32_t strips = 0, bands = 0, band_rows = 0, K = 0;
         uint32_t* flags = nullptr;
         uint32_t flag_base = 0;
+        bool coop = true;  // cooperative launch (GOL_DEV_RES_PLAIN=1: plain, dev A/B)
         hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering with the shared stream
     } res;
 
@@ -1341,6 +1342,10 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
     HIP_TRY(hipEventCreateWithFlags(&e->res.ev_in, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->res.ev_out, hipEventDisableTiming));
     e->res.on = true;
+    {
+        const char* v = std::getenv("GOL_DEV_RES_PLAIN");
+        e->res.coop = !(v && std::atoi(v) == 1);
+    }
     e->K = (uint32_t)e->res.K;
     return GOL_OK;
 }
@@ -1397,7 +1402,7 @@ gol_status step_resident(gol_engine* e, uint64_t generations)
 #endif
         hipEvent_t e0, e1;
         GOL_TRY(timing_begin(e, rs, &e0, &e1));
-        HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, rs));
+        HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, rs, r.coop));
         // lanes process every held row of every tile, every generation
         const double comp = (double)g * r.bands * r.strips * gol::kResWaves * r.rows * 64.0 * 64.0;
         GOL_TRY(timing_end(e, rs, e0, e1, (double)e->H * (double)e->W * g, comp));

@@ -427,15 +427,33 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
 #endif
 }
 
+// Cooperative launch: every tile waits for its neighbours, so all of them must be
+// resident at once.  The planner keeps the grid within the occupancy query x CUs;
+// hipLaunchCooperativeKernel checks it again at launch time against what the
+// device can actually hold (CU masking, another process's kernels) and refuses
+// (hipErrorCooperativeLaunchTooLarge, reported by gol_step) instead of letting
+// queued tiles run the neighbours' bounded waits out.
+template <int M, int RULE>
+hipError_t launch_res_coop(const ResArgs& a, int grid, hipStream_t s, bool coop)
+{
+    if (!coop) {
+        hipLaunchKernelGGL((life_res_kernel<M, RULE>), dim3(grid), dim3(64 * kResWaves), 0, s, a);
+        return hipGetLastError();
+    }
+    ResArgs args = a;
+    void* params[] = {&args};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&life_res_kernel<M, RULE>),
+                                      dim3(grid), dim3(64 * kResWaves), params, 0, s);
+}
+
 template <int M>
-hipError_t launch_res_m(const ResArgs& a, RuleKind rule, int grid, hipStream_t s)
+hipError_t launch_res_m(const ResArgs& a, RuleKind rule, int grid, hipStream_t s, bool coop)
 {
     switch (rule) {
-    case RULE_REF: hipLaunchKernelGGL((life_res_kernel<M, RULE_REF>), dim3(grid), dim3(64 * kResWaves), 0, s, a); break;
-    case RULE_CONWAY: hipLaunchKernelGGL((life_res_kernel<M, RULE_CONWAY>), dim3(grid), dim3(64 * kResWaves), 0, s, a); break;
-    default: hipLaunchKernelGGL((life_res_kernel<M, RULE_GENERIC>), dim3(grid), dim3(64 * kResWaves), 0, s, a); break;
+    case RULE_REF: return launch_res_coop<M, RULE_REF>(a, grid, s, coop);
+    case RULE_CONWAY: return launch_res_coop<M, RULE_CONWAY>(a, grid, s, coop);
+    default: return launch_res_coop<M, RULE_GENERIC>(a, grid, s, coop);
     }
-    return hipGetLastError();
 }
 
 template <int M>
@@ -453,14 +471,15 @@ int occupancy_res_m(RuleKind rule)
 
 }  // namespace
 
-hipError_t launch_resident(const ResArgs& a, int rows, RuleKind rule, int grid, hipStream_t s)
+hipError_t launch_resident(const ResArgs& a, int rows, RuleKind rule, int grid, hipStream_t s,
+                           bool coop)
 {
     switch (rows) {
-    case 2: return launch_res_m<2>(a, rule, grid, s);
-    case 3: return launch_res_m<3>(a, rule, grid, s);
-    case 4: return launch_res_m<4>(a, rule, grid, s);
-    case 6: return launch_res_m<6>(a, rule, grid, s);
-    case 8: return launch_res_m<8>(a, rule, grid, s);
+    case 2: return launch_res_m<2>(a, rule, grid, s, coop);
+    case 3: return launch_res_m<3>(a, rule, grid, s, coop);
+    case 4: return launch_res_m<4>(a, rule, grid, s, coop);
+    case 6: return launch_res_m<6>(a, rule, grid, s, coop);
+    case 8: return launch_res_m<8>(a, rule, grid, s, coop);
     default: return hipErrorInvalidValue;
     }
 }

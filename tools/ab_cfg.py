@@ -36,8 +36,16 @@ def main():
         engines = []
         for c in cfgs:
             kw = dict(rule=rule, device=0, streams=1, resident=1)
-            kw.update(c)
+            kw.update({k: v for k, v in c.items() if k != "env"})
+            env = c.get("env", {})  # environment at create (dev knobs)
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update({k: str(v) for k, v in env.items()})
             e = pkg.Engine(h, w, **kw)
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
             e.init_random(1)
             e.step(a.gens)
             e.sync()
