@@ -259,7 +259,11 @@ struct gol_engine {
         int32_t strips = 0, bands = 0, band_rows = 0, K = 0;
         uint32_t* flags = nullptr;
         uint32_t flag_base = 0;
-        bool coop = true;  // cooperative launch (GOL_DEV_RES_PLAIN=1: plain, dev A/B)
+        // hipLaunchCooperativeKernel (GOL_DEV_RES_COOP=1): the device re-checks that
+        // every tile fits at once, but the launch costs ~30 us more (C2: 640 vs
+        // 609-614 us per 1000 generations, profiles/r03/ab_resident_coop.jsonl);
+        // the planner's occupancy check and the bounded waits cover it by default
+        bool coop = false;
         hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering with the shared stream
     } res;
 
@@ -1343,8 +1347,8 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
     HIP_TRY(hipEventCreateWithFlags(&e->res.ev_out, hipEventDisableTiming));
     e->res.on = true;
     {
-        const char* v = std::getenv("GOL_DEV_RES_PLAIN");
-        e->res.coop = !(v && std::atoi(v) == 1);
+        const char* v = std::getenv("GOL_DEV_RES_COOP");
+        e->res.coop = v && std::atoi(v) == 1;
     }
     e->K = (uint32_t)e->res.K;
     return GOL_OK;

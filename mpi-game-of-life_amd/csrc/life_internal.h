@@ -185,9 +185,9 @@ struct ResArgs {
     uint32_t birth, survive;
     uint64_t* wlog;       // dev timing builds only (GOL_EXP & 2048): 4 words per wavefront
 };
-// coop: hipLaunchCooperativeKernel (the default; false = a plain launch, dev A/B)
+// coop: hipLaunchCooperativeKernel, else a plain launch (engine.cpp Resident::coop)
 hipError_t launch_resident(const ResArgs& a, int rows, RuleKind rule, int grid, hipStream_t s,
-                           bool coop = true);
+                           bool coop = false);
 int resident_blocks_per_cu(int rows, RuleKind rule);
 
 // Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field

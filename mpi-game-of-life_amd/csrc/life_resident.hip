@@ -427,12 +427,13 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
 #endif
 }
 
-// Cooperative launch: every tile waits for its neighbours, so all of them must be
-// resident at once.  The planner keeps the grid within the occupancy query x CUs;
-// hipLaunchCooperativeKernel checks it again at launch time against what the
-// device can actually hold (CU masking, another process's kernels) and refuses
-// (hipErrorCooperativeLaunchTooLarge, reported by gol_step) instead of letting
-// queued tiles run the neighbours' bounded waits out.
+// Every tile waits for its neighbours, so all of them must be resident at once.
+// The planner keeps the grid within the occupancy query x CUs (one tile per CU);
+// with `coop`, hipLaunchCooperativeKernel checks it again at launch time against
+// what the device can actually hold (CU masking, another process's kernels) and
+// refuses (hipErrorCooperativeLaunchTooLarge, reported by gol_step) instead of
+// letting queued tiles run the neighbours' bounded waits out -- at ~30 us per
+// launch, so it is opt-in (engine.cpp Resident::coop).
 template <int M, int RULE>
 hipError_t launch_res_coop(const ResArgs& a, int grid, hipStream_t s, bool coop)
 {

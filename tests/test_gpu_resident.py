@@ -159,3 +159,21 @@ def test_two_resident_engines_interleaved(pkg, oracle):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+def test_resident_cooperative_launch(pkg, oracle, monkeypatch, rule):
+    """GOL_DEV_RES_COOP=1: the same kernel through hipLaunchCooperativeKernel (the
+    device re-checks that every tile is resident at once), multi-strip rows and
+    two launches carrying the epoch flags, against the oracle."""
+    monkeypatch.setenv("GOL_DEV_RES_COOP", "1")
+    h, w = 1000, 5000
+    R = rules(oracle)[rule]
+    g = oracle.bp_random(h, w, 21)
+    with pkg.Engine(h, w, rule=R, device=0, resident=2) as e:
+        assert e.resident is not None
+        e.init_random(21)
+        e.step(37)
+        e.step(40)
+        got = e.store_packed()
+    assert (got == oracle.bp_run(g, w, 77, R)).all()
