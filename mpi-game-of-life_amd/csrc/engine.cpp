@@ -244,6 +244,7 @@ struct gol_engine {
         SegDesc* dev = nullptr;
     };
     std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: see RankGeom
+    std::vector<std::vector<Plan>> plan_alts;  // autotuner candidates per plan (build_plans)
 
     // row-block hand-off buffers (life_stencil.h): region 0 serves launches on
     // `stream`, region 1 those on `band_stream` (the two may run concurrently)
@@ -529,11 +530,13 @@ struct Skew {
 };
 
 Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, int occ, int K,
-              int planes, bool hand, int64_t max_units = INT64_MAX, int64_t half_stride = 0)
+              int planes, bool hand, int64_t max_units = INT64_MAX, int64_t half_stride = 0,
+              double rho_mult = 1.0)
 {
     Skew best_s;
     double rho = hand ? kAgeRateHand : kAgeRateClassic;
     if (const char* v = std::getenv("GOL_DEV_AGE_SKEW")) rho = std::atof(v);
+    rho *= rho_mult;
     const int64_t rows = sg.out_hi - sg.out_lo;
     if (rho <= 0 || rho >= 1 || occ != 2 || rows <= 0) return best_s;
     const int pf = gol::prefetch_of(K, planes);
@@ -649,6 +652,14 @@ bool single_stream_skews(uint64_t h, uint64_t w, const gol_config* cfg)
     return false;
 }
 
+void free_plan(gol_engine::Plan& q)
+{
+    if (q.dev) (void)hipFree(q.dev);
+    if (q.dpairs) (void)hipFree(q.dpairs);
+    q.dev = nullptr;
+    q.dpairs = nullptr;
+}
+
 gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
 {
     int cus = 0;
@@ -664,10 +675,10 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     const char* dev_pairs = std::getenv("GOL_DEV_PAIRS");
     const int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) ? 0 : (int64_t)e->stride;
     auto units_of = [&](const std::vector<SegDesc>& segs, int32_t groups, int shift, int64_t R,
-                        bool hand) {
+                        bool hand, int64_t hs_v) {
         int64_t u = plan_units(segs, groups);
-        if (hs && shift == 0 && segs.size() == 1 && col_layout((int64_t)e->ng, true).half())
-            u += half_units(segs[0], half_rows_for(R, hand, (int)e->K), (int)e->K, e->planes, hs,
+        if (hs_v && shift == 0 && segs.size() == 1 && col_layout((int64_t)e->ng, true).half())
+            u += half_units(segs[0], half_rows_for(R, hand, (int)e->K), (int)e->K, e->planes, hs_v,
                             nullptr);
         return u;
     };
@@ -713,9 +724,12 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
             handoff = 1;
         }
     }
-    for (size_t pi = 0; pi < raw.size(); ++pi) {
+    // One launch plan for raw plan pi into p: hs_v the half strip's row stride (0 =
+    // none), rho_mult scales the skew's young/old rate, kind the engine's block
+    // kind (1 classic, 2 hand-off).  The autotuner's variants come from here too.
+    auto build_one = [&](size_t pi, int64_t hs_v, double rho_mult, uint32_t kind,
+                         gol_engine::Plan& p) -> gol_status {
         const auto& r = raw[pi];
-        gol_engine::Plan p;
         p.segs = r;
         // the band launch runs beside the interior launch: classic blocks, so that
         // at most one launch that waits for its own wavefronts runs at a time
@@ -723,7 +737,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         const bool inner = e->overlap && pi == (size_t)e->Hx + 1;
         const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
                                               (int)e->rows_per_wave, e->lane_shift,
-                                              band ? 1u : handoff, hs);
+                                              band ? 1u : kind, hs_v);
         p.rpw = rp.rpw;
         p.groups = rp.groups;
         p.lane_shift = rp.lane_shift;
@@ -744,7 +758,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
             p.hand = false;
         }
         finish_segs(p.segs, p.rpw, p.groups);
-        p.total_units = units_of(p.segs, p.groups, p.lane_shift, p.rpw, p.hand);
+        p.total_units = units_of(p.segs, p.groups, p.lane_shift, p.rpw, p.hand, hs_v);
         int64_t cap = INT64_MAX;
         if (inner && !e->rows_per_wave && !e->shared_device) {
             const int occ = p.hand ? occ_h : occ_c;
@@ -756,28 +770,29 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                     ++R;
                     if (p.hand && !handoff_fits(R, (int)e->K, e->planes)) continue;
                     finish_segs(segs, R, p.groups);
-                } while (units_of(segs, p.groups, p.lane_shift, R, p.hand) > cap && R < 4096);
+                } while (units_of(segs, p.groups, p.lane_shift, R, p.hand, hs_v) > cap && R < 4096);
                 p.rpw = R;
                 p.segs = segs;
-                p.total_units = units_of(p.segs, p.groups, p.lane_shift, p.rpw, p.hand);
+                p.total_units = units_of(p.segs, p.groups, p.lane_shift, p.rpw, p.hand, hs_v);
             }
         }
         if (!band && p.segs.size() == 1 && !e->rows_per_wave && !e->shared_device) {
             const int occ = p.hand ? occ_h : occ_c;
             const int64_t first = slots_first;
             Skew sk = age_skew(p.segs[0], p.rpw, p.groups, first, occ, (int)e->K, e->planes,
-                               p.hand, cap, p.lane_shift == 0 ? hs : 0);
+                               p.hand, cap, p.lane_shift == 0 ? hs_v : 0, rho_mult);
             // Auto block kind, per plan: hand-off lengths are confined to two classes
             // mod the prefetch block, which can leave a launch without a close
             // one-round fit (8416 rows in 113 blocks of 86/62 rows: 90 vs 77 us); a
             // skewed classic plan is taken when the model says it is faster.
-            if (p.hand && e->handoff == 0) {
+            if (p.hand && e->handoff == 0 && kind == handoff) {
                 const RowPlan rc = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h,
-                                                      4 * cus, 0, e->lane_shift, 1u, hs);
+                                                      4 * cus, 0, e->lane_shift, 1u, hs_v);
                 std::vector<SegDesc> cs = r;
                 finish_segs(cs, rc.rpw, rc.groups);
                 const Skew skc = age_skew(cs[0], rc.rpw, rc.groups, first, occ_c, (int)e->K,
-                                          e->planes, false, cap, rc.lane_shift == 0 ? hs : 0);
+                                          e->planes, false, cap, rc.lane_shift == 0 ? hs_v : 0,
+                                          rho_mult);
                 if (!rc.hand && skc.rows_old &&
                     (!sk.rows_old || skc.t < sk.t * kHandSkewCost)) {
                     p.hand = false;
@@ -802,7 +817,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         // half strip into units after the full strips' (young waves, blocks as long
         // as the young ones)
         if (p.lane_shift == 0) {
-            const ColLayout cl = col_layout((int64_t)e->ng, hs && p.segs.size() == 1);
+            const ColLayout cl = col_layout((int64_t)e->ng, hs_v && p.segs.size() == 1);
             p.edge = 1;
             if (p.groups != cl.strips) {  // a planner's fallback plan: equal blocks
                 p.groups = cl.strips;
@@ -815,7 +830,8 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                 p.half_q0 = cl.half_q0;
                 p.half_hi = cl.half_hi;
                 p.half_rows = half_rows_for(p.rpw, p.hand, (int)e->K);
-                p.pair_units = half_units(p.segs[0], p.half_rows, (int)e->K, e->planes, hs, &p.pairs);
+                p.pair_units = half_units(p.segs[0], p.half_rows, (int)e->K, e->planes, hs_v,
+                                          &p.pairs);
                 p.total_units += p.pair_units;
                 HIP_TRY(hipMalloc(&p.dpairs, sizeof(int64_t) * p.pairs.size()));
                 HIP_TRY(hipMemcpy(p.dpairs, p.pairs.data(), sizeof(int64_t) * p.pairs.size(),
@@ -859,7 +875,47 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * dsegs.size()));
         HIP_TRY(hipMemcpy(p.dev, dsegs.data(), sizeof(SegDesc) * dsegs.size(),
                           hipMemcpyHostToDevice));
+        return GOL_OK;
+    };
+    // Autotuner candidates (autotune_plans): for the plans of full-depth launches of
+    // an engine alone on its device, variants the row-cost models rank within their
+    // error -- without the half strip, the skew rate x 0.95 / 1.05, the other block
+    // kind -- are timed on the GPU after planning, and the fastest stays.
+    // GOL_DEV_AUTOTUNE=0 keeps the models' plans.
+    const char* dev_tune = std::getenv("GOL_DEV_AUTOTUNE");
+    const bool tune = !(dev_tune && std::atoi(dev_tune) == 0) && !e->rows_per_wave &&
+                      !e->shared_device;
+    auto same_plan = [](const gol_engine::Plan& a, const gol_engine::Plan& b) {
+        return a.hand == b.hand && a.rpw == b.rpw && a.rows_old == b.rows_old &&
+               a.rows_young == b.rows_young && a.groups == b.groups &&
+               a.pair_units == b.pair_units && a.segs[0].nblk == b.segs[0].nblk;
+    };
+    e->plan_alts.assign(raw.size(), {});
+    for (size_t pi = 0; pi < raw.size(); ++pi) {
+        gol_engine::Plan p;
+        GOL_TRY(build_one(pi, hs, 1.0, handoff, p));
         e->plans.push_back(p);
+        const bool full = e->nranks > 1 ? (pi < (size_t)e->Hx && (pi + 1) % e->K == 0) : pi == 0;
+        if (!tune || !full || p.segs.size() != 1 || p.lane_shift != 0 || !p.rows_old) continue;
+        struct Variant {
+            int64_t hs;
+            double rho;
+            uint32_t kind;
+        };
+        std::vector<Variant> vs = {{0, 1.0, handoff}, {hs, 0.95, handoff}, {hs, 1.05, handoff}};
+        if (e->handoff == 0 && gol::handoff_kernel_exists((int)e->K, e->rule))
+            vs.push_back({hs, 1.0, p.hand ? 1u : 2u});
+        for (const Variant& v : vs) {
+            gol_engine::Plan q;
+            GOL_TRY(build_one(pi, v.hs, v.rho, v.kind, q));
+            bool dup = q.segs.size() != 1 || same_plan(q, p);
+            for (const auto& o : e->plan_alts[pi]) dup = dup || same_plan(q, o);
+            if (dup) {
+                free_plan(q);
+                continue;
+            }
+            e->plan_alts[pi].push_back(q);
+        }
     }
     HIP_TRY(hipMalloc(&e->d_err, sizeof(int)));
 #if GOL_EXP
@@ -1056,6 +1112,7 @@ void step_schedule(uint32_t K, uint64_t Hx, bool overlap, bool halo_fresh, uint6
 }
 
 gol_status plan_resident(gol_engine* e, const gol_config* cfg);
+gol_status autotune_plans(gol_engine* e);
 
 // Kernels that wait for other wavefronts of their own launch -- hand-off row blocks
 // (life_stencil.h) and the resident kernel -- need every wavefront they wait for
@@ -1212,6 +1269,7 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         if (!off && reg.hand) c.resident = 1;
         st = build_plans(e, raw);
         if (st == GOL_OK) st = plan_resident(e, &c);
+        if (st == GOL_OK) st = autotune_plans(e);
         if (st == GOL_OK && !off) {
             WaitReg& r = g_wait_reg[e->device];
             if (e->res.on) {
@@ -1491,6 +1549,70 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     }
     if (swap) e->cur ^= 1;
     return GOL_OK;
+}
+
+// Autotuner (candidates from build_plans): each full-depth plan and its variants
+// run interleaved on the engine's buffers, 1 + 3 launches each timed with HIP
+// events (the stencil's time does not depend on the cells); the fastest by its
+// best launch replaces the models' plan if it is at least 1% faster.  The
+// variants are all plan kinds the parity tests pin, so this changes speed only.
+// 8-way rank launch shapes (one process, TCUPS, models' plan vs best variant,
+// profiles/r03/ab_rank_shapes_candidates.jsonl): 8224 rows 103.4 vs 107.7, 8608
+// 106.9 vs 115.6, 8672 106.7 vs 113.6.  A resident engine drops its candidates.
+gol_status check_err(gol_engine* e);
+
+gol_status autotune_plans(gol_engine* e)
+{
+    bool any = false;
+    for (const auto& a : e->plan_alts) any = any || !a.empty();
+    if (!any) return GOL_OK;
+    if (e->res.on) {
+        for (auto& a : e->plan_alts) {
+            for (auto& q : a) free_plan(q);
+            a.clear();
+        }
+        return GOL_OK;
+    }
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    HIP_TRY(hipEventCreate(&t0));
+    HIP_TRY(hipEventCreate(&t1));
+    gol_status st = GOL_OK;
+    for (size_t pi = 0; pi < e->plan_alts.size() && st == GOL_OK; ++pi) {
+        auto& alts = e->plan_alts[pi];
+        if (alts.empty()) continue;
+        std::vector<gol_engine::Plan> cand{e->plans[pi]};
+        cand.insert(cand.end(), alts.begin(), alts.end());
+        alts.clear();
+        std::vector<float> best(cand.size(), 1e30f);
+        for (int rep = 0; rep < 4 && st == GOL_OK; ++rep)
+            for (size_t c = 0; c < cand.size() && st == GOL_OK; ++c) {
+                e->plans[pi] = cand[c];
+                float ms = 0;
+                if (hipEventRecord(t0, e->stream) != hipSuccess) st = fail(GOL_EHIP, "autotune event");
+                if (st == GOL_OK) st = launch(e, (int)pi, e->K, false);
+                if (st == GOL_OK && (hipEventRecord(t1, e->stream) != hipSuccess ||
+                                     hipEventSynchronize(t1) != hipSuccess ||
+                                     hipEventElapsedTime(&ms, t0, t1) != hipSuccess))
+                    st = fail(GOL_EHIP, "autotune timing");
+                if (rep > 0) best[c] = std::min(best[c], ms);
+            }
+        size_t pick = 0;
+        for (size_t c = 1; c < cand.size(); ++c)
+            if (best[c] < best[pick] && best[c] < 0.99f * best[0]) pick = c;
+        e->plans[pi] = cand[pick];
+        for (size_t c = 0; c < cand.size(); ++c)
+            if (c != pick) free_plan(cand[c]);
+        if (std::getenv("GOL_DEV_PLANS"))
+            std::fprintf(stderr, "autotune plan %zu: candidate %zu of %zu (%.1f us vs %.1f us), R %lld, "
+                         "hand %d, skew %d/%d, half-strip units %lld\n", pi, pick, cand.size(),
+                         1e3 * best[pick], 1e3 * best[0], (long long)e->plans[pi].rpw,
+                         (int)e->plans[pi].hand, e->plans[pi].rows_old, e->plans[pi].rows_young,
+                         (long long)e->plans[pi].pair_units);
+    }
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    if (st == GOL_OK) st = check_err(e);  // a hand-off wait that timed out is a failure here too
+    return st;
 }
 
 // Order everything the side streams of a stripe engine have enqueued (band
@@ -1952,6 +2074,11 @@ void gol_destroy(gol_engine* e)
         if (p.dev) (void)hipFree(p.dev);
         if (p.dpairs) (void)hipFree(p.dpairs);
     }
+    for (auto& alts : e->plan_alts)
+        for (auto& p : alts) {
+            if (p.dev) (void)hipFree(p.dev);
+            if (p.dpairs) (void)hipFree(p.dpairs);
+        }
     for (int b = 0; b < 2; ++b) {
         if (e->alloc[b]) (void)hipFree(e->alloc[b]);
         if (e->side[b]) (void)hipFree(e->side[b]);

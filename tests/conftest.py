@@ -9,6 +9,12 @@ if ROOT not in sys.path:
 
 import __graft_entry__ as entry  # noqa: E402
 
+# Plans as the cost models choose them: the engine's autotuner (engine.cpp
+# autotune_plans) times variants at create and may pick another, equally exact
+# one; tests that pin plan properties need the models' choice.  The autotuner
+# itself is covered in test_gpu_autotune.py.
+os.environ.setdefault("GOL_DEV_AUTOTUNE", "0")
+
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 

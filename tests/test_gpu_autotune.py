@@ -1,0 +1,66 @@
+"""GPU parity of autotuned plans (engine.cpp build_plans variants +
+autotune_plans).
+
+At create, an engine alone on its device times the cost models' plan of every
+full-depth launch against a few variants (no half strip, skew rate x 0.95 /
+1.05, the other block kind) and keeps the fastest.  Every variant is a plan kind
+the other tests pin; here the autotuned engines are checked bit-exact against
+the oracle and against the models' plans at the rank launch shapes where the
+variants differ most, and through the rank round schedule over RCCL.
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+W = 65536
+THREADS = 16
+
+
+@pytest.fixture
+def autotune(monkeypatch):
+    monkeypatch.setenv("GOL_DEV_AUTOTUNE", "1")
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+@pytest.mark.parametrize("h", [8224, 8608])
+def test_autotuned_stripe_vs_oracle(pkg, oracle, autotune, h, rule):
+    R = oracle.REF_RULE if rule == "ref" else oracle.CONWAY
+    gens = 2 * 16 + 3
+    with pkg.Engine(h, W, rule=R, device=0, streams=1) as e:
+        e.init_random(9)
+        e.step(gens)
+        got = e.digest()
+    g = oracle.bp_run(oracle.bp_random(h, W, 9), W, gens, R, threads=THREADS)
+    assert got == oracle.bp_digest(g, W)
+
+
+def test_autotuned_equals_model_plans_c3(pkg, autotune, monkeypatch):
+    """65536^2, Conway over several launches: autotuned vs the models' plan."""
+    gens = 3 * 16 + 5
+    with pkg.Engine(W, W, rule=pkg.CONWAY, device=0) as e:
+        e.init_random(4)
+        e.step(gens)
+        got = e.digest()
+    monkeypatch.setenv("GOL_DEV_AUTOTUNE", "0")
+    with pkg.Engine(W, W, rule=pkg.CONWAY, device=0) as e:
+        e.init_random(4)
+        e.step(gens)
+        assert e.digest() == got
+
+
+def test_autotuned_rank_shape(pkg, monkeypatch):
+    """The 8-way C4 rank (8192 own rows + 2 x 256 halo rows, 16 full-depth plans
+    autotuned) over RCCL self-loops, against the models' plans (same field after
+    two rounds and a partial one)."""
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    n, world, rank, gens = 65536, 8, 3, 2 * 256 + 40
+    out = []
+    for tune in ("1", "0"):
+        monkeypatch.setenv("GOL_DEV_AUTOTUNE", tune)
+        with pkg.Engine(n, n, rule=pkg.CONWAY, device=0, rank=rank, nranks=world,
+                        uid=pkg.unique_id()) as e:
+            e.init_random(3)
+            e.step(gens)
+            out.append((e.digest(), e.store_packed()))
+    assert out[0][0] == out[1][0]
+    assert (out[0][1] == out[1][1]).all()
