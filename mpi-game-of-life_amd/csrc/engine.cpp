@@ -635,7 +635,8 @@ bool single_stream_skews(uint64_t h, uint64_t w, const gol_config* cfg)
     SegDesc s{};
     s.in_rows = s.field_h = s.out_hi = (int64_t)h;
     const char* dev_pairs = std::getenv("GOL_DEV_PAIRS");
-    const int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) ? 0 : (int64_t)(ng * G);
+    const int64_t hs =
+        (dev_pairs && std::atoi(dev_pairs) == 0) || h >= (1ull << 30) ? 0 : (int64_t)(ng * G);
     for (int hand = 0; hand <= 1; ++hand) {
         if ((hand && (cfg->handoff == 1 || !hand_ok)) || (!hand && cfg->handoff == 2)) continue;
         const RowPlan rp = pick_rows_per_wave({s}, ng, K, planes, occ_c, occ_h, 4 * cus, 0, shift,
@@ -672,8 +673,11 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     bool any_hand = false;
     // the packed half strip of one-segment plans (col_layout; GOL_DEV_PAIRS=0 turns
     // it off for A/B): the planners count its units
+    // (the kernel reads the half strip's row numbers as 32-bit: buffers up to 2^30 rows)
     const char* dev_pairs = std::getenv("GOL_DEV_PAIRS");
-    const int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) ? 0 : (int64_t)e->stride;
+    const int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) || e->buf_rows >= (1ull << 30)
+                           ? 0
+                           : (int64_t)e->stride;
     auto units_of = [&](const std::vector<SegDesc>& segs, int32_t groups, int shift, int64_t R,
                         bool hand, int64_t hs_v) {
         int64_t u = plan_units(segs, groups);
