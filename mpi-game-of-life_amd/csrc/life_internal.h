@@ -123,11 +123,12 @@ constexpr int warm_steps_of(int K, int planes)
 {
     return (2 * K + prefetch_of(K, planes) - 1) / prefetch_of(K, planes) * prefetch_of(K, planes);
 }
-// Tail offsets with a hand-off kernel: 0 and prefetch/2, and 6 with the 8-step
-// prefetch block (offset 2 there needs 258 VGPRs: one wave per SIMD).
+// Tail offsets with a hand-off kernel: 0 and prefetch/2, and 2 and 6 with the
+// 8-step prefetch block (offset 2 there would take 258 VGPRs, one wave per SIMD:
+// it is built capped at 256, GOL_TOFF2_CAP).
 constexpr bool handoff_toff_exists(int off, int pf)
 {
-    return off == 0 || off == pf / 2 || (pf == 8 && off == 6);
+    return off == 0 || off == pf / 2 || (pf == 8 && (off == 6 || off == 2));
 }
 // A consumer block of R rows streams R + 2 input steps after the warm-up, i.e.
 // (R + 2 - warm) mod prefetch must be an offset with a kernel, and at least two

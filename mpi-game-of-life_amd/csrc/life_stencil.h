@@ -326,7 +326,10 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2;
 #endif
 
 template <int K, int RULE, int NP, bool HAND, int TOFF>
-__global__ __launch_bounds__(256) void life_tb_kernel(StepArgs a)
+// (the 8-step-prefetch hand-off kernels of tail offset 2 need 258 VGPRs: capped to
+// keep 2 waves per SIMD, with a few scratch spills)
+__global__ __launch_bounds__(256, (HAND && TOFF == 2 && kPfOf<NP, K>() == 8 && RULE != RULE_GENERIC) ? 2 : 1)
+void life_tb_kernel(StepArgs a)
 {
     constexpr bool kBirths = RULE != RULE_REF;
     constexpr int G = NP / 2;  // words per lane group
@@ -823,12 +826,14 @@ hipError_t launch_planes(const StepArgs& a, RuleKind rule, bool hand, hipStream_
 {
     if constexpr (K >= kHandoffMinDepth) {
         if (hand) {
-            // tail offsets 0, pf/2 and (pf = 8) 6: handoff_toff_exists
+            // tail offsets 0, pf/2 and (pf = 8) 2, 6: handoff_toff_exists
             constexpr int pf = kPfOf<NP, K>();
             if (a.tail_off == 0) return launch_kernel<K, NP, true, 0>(a, rule, s);
             if (a.tail_off == pf / 2) return launch_kernel<K, NP, true, pf / 2>(a, rule, s);
-            if constexpr (pf == 8)
+            if constexpr (pf == 8) {
                 if (a.tail_off == 6) return launch_kernel<K, NP, true, (pf == 8 ? 6 : 0)>(a, rule, s);
+                if (a.tail_off == 2) return launch_kernel<K, NP, true, (pf == 8 ? 2 : 0)>(a, rule, s);
+            }
             return hipErrorInvalidValue;
         }
     }

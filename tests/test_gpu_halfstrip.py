@@ -101,11 +101,11 @@ def test_block_kind_policy(pkg, h, hand, half):
 
 
 @pytest.mark.parametrize("rule", ["ref", "conway"])
-@pytest.mark.parametrize("R,toff", [(62, 0), (66, 4), (68, 6)])
+@pytest.mark.parametrize("R,toff", [(62, 0), (64, 2), (66, 4), (68, 6)])
 def test_handoff_tail_offsets_vs_oracle(pkg, oracle, R, toff, rule):
-    """Hand-off blocks of every tail offset with a kernel at depth 16 (0, 4 and,
-    r03, 6: (R + 2 - 32) mod 8), with the half strip (8192 columns: a 2-group
-    gap), two launches and a remainder, against the oracle."""
+    """Hand-off blocks of every tail offset at depth 16 (0, 4 and, r03, 2 and 6:
+    (R + 2 - 32) mod 8), with the half strip (8192 columns: a 2-group gap), two
+    launches and a remainder, against the oracle."""
     assert (R + 2 - 32) % 8 == toff
     h, w, gens, seed = 900, 8192, 2 * 16 + 5, 13
     Rr = rule_of(pkg, rule)
