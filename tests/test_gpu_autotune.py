@@ -64,3 +64,25 @@ def test_autotuned_rank_shape(pkg, monkeypatch):
             out.append((e.digest(), e.store_packed()))
     assert out[0][0] == out[1][0]
     assert (out[0][1] == out[1][1]).all()
+
+
+def test_autotune_respects_waiting_kernel_registry(pkg, oracle, autotune):
+    """Two default engines at a hand-off shape on one GPU, both autotuned: the
+    second (device's hand-off slot taken) gets no hand-off variant, and both fields
+    stay exact when stepped without syncs in between."""
+    h, gens = 8448, 40
+    want = oracle.bp_digest(oracle.bp_run(oracle.bp_random(h, W, 5), W, gens, oracle.CONWAY,
+                                          threads=THREADS), W)
+    a = pkg.Engine(h, W, rule=pkg.CONWAY, device=0)
+    b = pkg.Engine(h, W, rule=pkg.CONWAY, device=0)
+    try:
+        assert not b.handoff
+        for e in (a, b):
+            e.init_random(5)
+        for _ in range(2):
+            a.step(gens // 2)
+            b.step(gens // 2)
+        assert a.digest() == want and b.digest() == want
+    finally:
+        a.close()
+        b.close()
