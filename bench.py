@@ -396,6 +396,8 @@ def main():
                 "halo_depth": eng.halo_depth, "rows_per_wave": eng.rows_per_wave,
                 "handoff": eng.handoff, "resident": eng.resident,
                 "age_skew": eng.age_skew,
+                # (strips per row block, half-strip wavefronts, half-strip lane groups)
+                "columns": list(eng.columns),
                 "parallelism": f"row-stripes x{world}" if world > 1 else "single GPU",
             },
             "roofline": {
