@@ -128,7 +128,9 @@ typedef struct gol_timing {
 /* Defaults: reference-effective rule, GLOBAL semantics, auto tuning. */
 void gol_config_init(gol_config* cfg);
 
-/* Replaces the allocation in readGridFromFile (:88-89).  h rows x w columns. */
+/* Replaces the allocation in readGridFromFile (:88-89).  h rows x w columns.
+ * An engine alone on its device times a few equally exact launch plans on its
+ * own buffers before returning (tens of ms) and keeps the fastest. */
 gol_status gol_create(uint64_t h, uint64_t w, const gol_config* cfg, gol_engine** out);
 
 /* Replaces readGridFromFile's parse (:91-99): buf holds the data.txt bytes,
