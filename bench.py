@@ -77,6 +77,8 @@ def parse():
     p.add_argument("--rule", default="ref", choices=["ref", "conway"])
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-sub-records", action="store_true",
+                   help="skip the B3/S23 65536^2 and C2 4096^2 lines after the headline")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = the allowed CPUs")
     return p.parse_args()
 
@@ -208,23 +210,33 @@ def ctl_device(dist):
 def rccl_selfcheck(pkg, dist, torch, world, rank, local):
     """N > 1: the RCCL halo path end to end on a small field before the timed run.
     Every rank advances its stripe of a 4096^2 B3/S23 field (rounds of Hx
-    generations with ncclSend/Recv exchanges) and the stripe digests are summed
-    (digests are order-independent sums, engine.cpp digest_kernel); rank 0 evolves
-    the whole field alone on its GPU and compares.  Not part of the timed region."""
+    generations with ncclSend/Recv exchanges); rank 0 evolves the whole field
+    alone on its GPU and compares, per rank, that rank's stripe digest with the
+    single engine's digest of the same rows (gol_digest_rows), and the sum of all
+    of them with the single engine's whole-field digest.  Each rank also reports
+    its communicator as RCCL sees it (gol_comm_info: ncclCommCount, user rank,
+    device, up/down peers), so that a first multi-GPU failure is diagnosable from
+    the record alone.  Not part of the timed region."""
     n, gens, seed = 4096, 3 * 64 + 21, 5
     uid = [pkg.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     with pkg.Engine(n, n, rule=pkg.CONWAY, device=local, rank=rank, nranks=world,
                     uid=uid[0]) as e:
         hx = e.halo_depth
+        row0, rows = e.row0, e.rows
+        try:
+            comm = e.comm_info()
+        except Exception as ex:  # noqa: BLE001 -- reported, not fatal here
+            comm = {"error": str(ex)}
         e.init_random(seed)
         e.step(gens)
-        live, hsh = e.digest()
+        mine = e.digest()
+    per = [None] * world
+    dist.all_gather_object(per, {"rank": rank, "row0": row0, "rows": rows,
+                                 "digest": list(mine), "comm": comm,
+                                 "device": local})
     mask = (1 << 64) - 1
-    t = torch.tensor([live, hsh - (1 << 64) if hsh >= (1 << 63) else hsh], dtype=torch.int64,
-                     device=ctl_device(dist))
-    dist.all_reduce(t)  # int64 sums wrap mod 2^64 like the digest's
-    got = (int(t[0].item()) & mask, int(t[1].item()) & mask)
+    got = (sum(p["digest"][0] for p in per) & mask, sum(p["digest"][1] for p in per) & mask)
     rec = {"field": f"{n}x{n}", "rule": "B3/S23", "generations": gens, "halo_depth": hx,
            "ranks": world}
     if rank == 0:
@@ -232,9 +244,75 @@ def rccl_selfcheck(pkg, dist, torch, world, rank, local):
             ref.init_random(seed)
             ref.step(gens)
             want = ref.digest()
-        rec["ok"] = got == want
+            for p in per:
+                w = ref.digest_rows(p["row0"], p["rows"])
+                p["want"] = list(w)
+                p["ok"] = tuple(p["digest"]) == w
+        rec["ok"] = got == want and all(p["ok"] for p in per)
         rec["digest"] = list(got)
+        rec["want"] = list(want)
+        rec["per_rank"] = per
     return rec
+
+
+def timed_steps(eng, gens, steps, warmup, world, dist, torch, timing_every=8):
+    """W untimed steps, then K steps between barrier + device sync brackets; HIP
+    events around every `timing_every`-th launch.  Returns (seconds, timing)."""
+    def barrier():
+        if world > 1:
+            dist.barrier()
+    for _ in range(warmup):
+        eng.step(gens)
+    eng.sync()
+    eng.set_timing(timing_every)
+    eng.reset_timing()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.step(gens)
+    eng.sync()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    return dt, eng.timing()
+
+
+def valu_frac(tm, rule):
+    """The stage logic's VALU issue slots per second of the sampled launches over
+    the spec issue rate (module docstring), and the work ratio."""
+    launches = max(tm["launches"], 1)
+    launch_s = tm["kernel_ms"] / launches / 1e3
+    cg = tm["cell_gens"] / launches
+    streams = max(1, tm.get("streams", 1))
+    achieved = cg / CELLS_PER_WAVE_INSTR * STAGE_SLOTS[rule] * streams / max(launch_s, 1e-12)
+    return (round(achieved / (SIMDS * SPEC_SLOT_RATE), 4),
+            round(tm["cell_gens_computed"] / max(tm["cell_gens"], 1), 4))
+
+
+def sub_record(pkg, torch, local, size, rule, gens, steps, warmup, seed):
+    """One more N = 1 configuration, timed like the headline (its own engine):
+    north_star's literal rule B3/S23 at 65536^2, or the C2 field 4096^2 (resident
+    kernel)."""
+    r = pkg.REF_RULE if rule == "ref" else pkg.CONWAY
+    with pkg.Engine(size, size, rule=r, device=local) as eng:
+        eng.init_random(seed)
+        dt, tm = timed_steps(eng, gens, steps, warmup, 1, None, torch)
+        frac, work = valu_frac(tm, rule)
+        return {
+            "workload": f"{size}x{size}, {gens} generations per step, "
+                        f"{'B/S2' if rule == 'ref' else 'B3/S23'}",
+            "value": round(float(size) * size * gens * steps / dt / 1e9, 2),
+            "unit": "GCUPS",
+            "steps": steps, "warmup": warmup,
+            "ms_per_step": round(dt / steps * 1e3, 3),
+            "kernel": "life_res_kernel" if eng.resident else "life_tb_kernel",
+            "avg_launch_ms": round(tm["kernel_ms"] / max(tm["launches"], 1), 4),
+            "valu_frac": frac,
+            "work_ratio": work,
+            "tb_depth": eng.tb_depth, "resident": eng.resident, "age_skew": eng.age_skew,
+            "autotune": list(eng.tuning),
+        }
 
 
 def main():
@@ -246,7 +324,9 @@ def main():
     # rank's engine talks RCCL to itself (engine.cpp gol_create_rank), ranks share
     # the GPUs there are, torch.distributed runs over gloo (RCCL refuses two ranks
     # of one communicator on one device), and rccl_selfcheck is expected to fail
-    # (a self-looped stripe is not the field's stripe)
+    # (a self-looped stripe is not the field's stripe).  Such a record carries
+    # "rehearsal": true, the physical GPU count, and `value` null (the rate is
+    # under "rehearsal_value"): it is never an N-GPU result.
     rehearsal = os.environ.get("GOL_DEV_RCCL_SELF") == "1"
     if world != a.gpus:
         if not (world == 1 and a.gpus == 1):
@@ -263,6 +343,7 @@ def main():
     torch.cuda.set_device(local)
     kw = dict(rule=rule, device=local, tb_depth=a.tb_depth, rows_per_wave=a.rows_per_wave,
               handoff=a.handoff)
+
     def barrier():
         if world > 1:
             dist.barrier()
@@ -273,6 +354,13 @@ def main():
         return pkg.Engine(n, n, halo_depth=a.halo_depth, rank=rank, nranks=world, uid=uid[0],
                           exchange_overlap=overlap, **kw)
 
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=ctl_device(dist))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     modes = None
     if world > 1:
         dist.init_process_group("gloo" if rehearsal else "nccl")
@@ -282,21 +370,8 @@ def main():
         # blocking one: the same K steps, reported beside `value`
         eng = rank_engine(2)
         eng.init_random(a.seed)
-        for _ in range(a.warmup):
-            eng.step(a.gens)
-        eng.sync()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            eng.step(a.gens)
-        eng.sync()
-        torch.cuda.synchronize()
-        barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                         device=ctl_device(dist))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ov_dt = float(t.item())
+        ov_dt, _ = timed_steps(eng, a.gens, a.steps, a.warmup, world, dist, torch, 0)
+        ov_dt = max_over_ranks(ov_dt)
         eng.close()
         modes = {"overlapped": {"value": round(float(n) * n * a.gens * a.steps / ov_dt / 1e9, 2),
                                 "ms_per_step": round(ov_dt / a.steps * 1e3, 3),
@@ -307,23 +382,9 @@ def main():
         selfcheck = None
     eng.init_random(a.seed)
 
-    for _ in range(a.warmup):
-        eng.step(a.gens)
-    eng.sync()
     # HIP events around every 8th launch: representative launch durations without
     # the per-event stream cost (~6 us) landing on every launch of the timed region
-    eng.set_timing(8)
-    eng.reset_timing()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        eng.step(a.gens)
-    eng.sync()
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    tm = eng.timing()
+    dt, tm = timed_steps(eng, a.gens, a.steps, a.warmup, world, dist, torch, 8)
     # The events above keep a single-stream engine off its hipGraph replay (the
     # default path without timing): one more step on that path, not part of
     # `value`, shows the two agree
@@ -338,16 +399,8 @@ def main():
         torch.cuda.synchronize()
         dt_graph = min(dt_graph, time.perf_counter() - t1)
     barrier()
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=ctl_device(dist))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        k = torch.tensor([tm["kernel_ms"] / max(tm["launches"], 1)], dtype=torch.float64,
-                         device=ctl_device(dist))
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-        avg_launch_ms = float(k.item())
-    else:
-        avg_launch_ms = tm["kernel_ms"] / max(tm["launches"], 1)
+    dt = max_over_ranks(dt)
+    avg_launch_ms = max_over_ranks(tm["kernel_ms"] / max(tm["launches"], 1))
 
     cell_gens = float(n) * n * a.gens * a.steps
     gcups = cell_gens / dt / 1e9
@@ -371,12 +424,25 @@ def main():
     ctr = counters_for(cfg_key) or {}
     insts = ctr.get("insts_valu_per_launch")
     traffic = ctr.get("hbm_bytes_per_launch")
+    tuning = eng.tuning
+    eng.close()
+
+    # north_star's literal rule (B3/S23) at 65536^2 and the C2 field (4096^2,
+    # resident kernel), timed after the headline on rank 0 at N = 1
+    subs = None
+    if world == 1 and not a.no_sub_records and n == 65536 and a.gens == 1000:
+        subs = {
+            ("conway_65536" if a.rule == "ref" else "ref_65536"): sub_record(pkg, torch, local, 65536,
+                                       "conway" if a.rule == "ref" else "ref", 1000, 3, 1, a.seed),
+            "c2_4096": sub_record(pkg, torch, local, 4096, a.rule, 1000, 3, 1, a.seed),
+        }
 
     if rank == 0:
         rec = {
             "metric": METRIC,
-            # a failed RCCL self-check voids the multi-GPU number
-            "value": round(gcups, 2) if (ok or rehearsal) else None,
+            # a failed RCCL self-check voids the multi-GPU number; a rehearsal on
+            # one GPU (self-looped RCCL) is never the N-GPU number
+            "value": round(gcups, 2) if (ok and not rehearsal) else None,
             "unit": "GCUPS",
             "n_gpus": world,
             "steps": a.steps,
@@ -398,6 +464,13 @@ def main():
                 "age_skew": eng.age_skew,
                 # (strips per row block, half-strip wavefronts, half-strip lane groups)
                 "columns": list(eng.columns),
+                # the plan the timed launches ran: the cost models' plan or the
+                # autotuner's variant, with the create-time best launch (us) of
+                # each (engine.cpp autotune_plans; rank 0's first full-depth plan)
+                "autotune": {"variant": tuning[0], "launch_us": tuning[1],
+                             "models_launch_us": tuning[2],
+                             "gain": (round(tuning[2] / tuning[1] - 1, 4)
+                                      if tuning[1] and tuning[2] else None)},
                 "parallelism": f"row-stripes x{world}" if world > 1 else "single GPU",
             },
             "roofline": {
@@ -435,14 +508,18 @@ def main():
                 "hbm_measured_frac": (round(traffic * streams / launch_s
                                             / (HBM_PEAK_GBPS * 1e9), 4) if traffic else None),
             },
+            "sub_records": subs,
             "cpu_baseline": None,
             "rccl_selfcheck": selfcheck,
             "exchange_modes": modes,
         }
+        if rehearsal:
+            rec["rehearsal"] = True
+            rec["rehearsal_value"] = round(gcups, 2)
+            rec["physical_gpus"] = torch.cuda.device_count()
         if world == 1 and not a.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(n, a.seed, a.cpu_threads)
         print(json.dumps(rec), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
     if rank == 0 and not ok and not rehearsal:

@@ -213,6 +213,20 @@ gol_status gol_plan_columns(gol_engine* e, uint32_t* strips, uint32_t* half_unit
  * NULL).  A composite engine reports 0. */
 gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint32_t* strips);
 
+/* The plan autotuner's outcome for the first full-depth launch plan (an engine
+ * alone on its device times a few variants of the cost models' plan at create
+ * and keeps one only if it is >= 3% faster): *variant 0 = the models' plan, else
+ * 1 + the index in {no_half_strip, skew_0.95, skew_1.05, other_block_kind};
+ * *tuned_us / *model_us = the best create-time launch of the plan that runs / of
+ * the models' plan (0 when nothing was timed).  Out pointers may be NULL. */
+gol_status gol_plan_tuning(gol_engine* e, uint32_t* variant, float* tuned_us, float* model_us);
+
+/* gol_digest restricted to field rows [row0, row0 + rows) (for a rank engine:
+ * the part of its own rows inside that range).  Lets one engine of the whole
+ * field check each rank's stripe separately. */
+gol_status gol_digest_rows(gol_engine* e, uint64_t row0, uint64_t rows, uint64_t* live,
+                           uint64_t* hash);
+
 /* ---- Multi-GPU, one process per GPU (replaces the MPI stripes :70-81 and the
  * halo exchange :104-145 with RCCL send/recv over xGMI) ---- */
 
@@ -228,6 +242,13 @@ gol_status gol_comm_unique_id(uint8_t id[128]);
  * it collectively with the same id.  cfg->semantics must be GLOBAL. */
 gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int rank,
                            int nranks, const uint8_t id[128], gol_engine** out);
+
+/* The RCCL communicator of a gol_create_rank engine as RCCL reports it
+ * (ncclCommCount, ncclCommUserRank, ncclCommCuDevice) and the engine's up/down
+ * peers (-1: no such neighbour).  Out pointers may be NULL.  GOL_ESTATE for an
+ * engine without a communicator. */
+gol_status gol_comm_info(gol_engine* e, int* count, int* rank, int* peer_up, int* peer_down,
+                         int* device);
 
 /* Halo transport supplied by the caller (host memory): the same rank engine,
  * partition and rounds as gol_create_rank, but each exchange stages the Hx

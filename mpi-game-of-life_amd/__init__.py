@@ -34,8 +34,12 @@ EXPORTS = [
     "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
     "gol_create_rank", "gol_create_group", "gol_group_step", "gol_plan_info",
     "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
-    "gol_plan_resident", "gol_plan_skew", "gol_plan_columns",
+    "gol_plan_resident", "gol_plan_skew", "gol_plan_columns", "gol_plan_tuning",
+    "gol_digest_rows", "gol_comm_info",
 ]
+
+# gol_plan_tuning's variants (engine.cpp kTuneVariantNames): 0 = the models' plan
+TUNE_VARIANTS = ["models", "no_half_strip", "skew_0.95", "skew_1.05", "other_block_kind"]
 
 
 class GolError(RuntimeError):
@@ -154,6 +158,11 @@ def lib():
     L.gol_plan_columns.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.gol_create_rank_transport.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32,
                                             ctypes.POINTER(Transport), ctypes.POINTER(vp)]
+    pf32 = ctypes.POINTER(ctypes.c_float)
+    L.gol_plan_tuning.argtypes = [vp, ctypes.POINTER(u32), pf32, pf32]
+    L.gol_digest_rows.argtypes = [vp, u64, u64, pu64, pu64]
+    pi32 = ctypes.POINTER(ctypes.c_int)
+    L.gol_comm_info.argtypes = [vp, pi32, pi32, pi32, pi32, pi32]
     L.gol_round_schedule.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32, u64, i32,
                                      ctypes.POINTER(SchedOp), u64, pu64, ctypes.POINTER(u32),
                                      ctypes.POINTER(u32)]
@@ -163,7 +172,8 @@ def lib():
                  "gol_reset_timing", "gol_info", "gol_rank_rows", "gol_comm_unique_id",
                  "gol_create_group", "gol_group_step", "gol_plan_info", "gol_plan_handoff",
                  "gol_plan_resident", "gol_plan_skew", "gol_plan_columns",
-                 "gol_create_rank_transport", "gol_round_schedule"]:
+                 "gol_create_rank_transport", "gol_round_schedule", "gol_plan_tuning",
+                 "gol_digest_rows", "gol_comm_info"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -284,6 +294,12 @@ class Engine:
         _check(lib().gol_plan_columns(self._h, ctypes.byref(st), ctypes.byref(hu), ctypes.byref(hg)))
         # (strips per row block, half-strip units, half-strip lane groups)
         self.columns = (st.value, hu.value, hg.value)
+        tv, tu, mu = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_float()
+        _check(lib().gol_plan_tuning(self._h, ctypes.byref(tv), ctypes.byref(tu), ctypes.byref(mu)))
+        # autotuner outcome of the first full-depth plan: (variant name, best launch us
+        # of the plan that runs, of the models' plan); us 0 = not timed
+        self.tuning = (TUNE_VARIANTS[tv.value] if tv.value < len(TUNE_VARIANTS) else str(tv.value),
+                       round(tu.value, 2), round(mu.value, 2))
 
     def close(self):
         if self._h:
@@ -336,6 +352,19 @@ class Engine:
         live, hsh = ctypes.c_uint64(), ctypes.c_uint64()
         _check(lib().gol_digest(self._h, ctypes.byref(live), ctypes.byref(hsh)))
         return live.value, hsh.value
+
+    def digest_rows(self, row0, rows):
+        """gol_digest over field rows [row0, row0 + rows) only."""
+        live, hsh = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().gol_digest_rows(self._h, row0, rows, ctypes.byref(live), ctypes.byref(hsh)))
+        return live.value, hsh.value
+
+    def comm_info(self):
+        """RCCL communicator of a rank engine: dict(count, rank, peer_up, peer_down,
+        device) as RCCL reports them (gol_comm_info)."""
+        v = [ctypes.c_int() for _ in range(5)]
+        _check(lib().gol_comm_info(self._h, *(ctypes.byref(x) for x in v)))
+        return dict(zip(("count", "rank", "peer_up", "peer_down", "device"), (x.value for x in v)))
 
     def set_timing(self, every=1):
         """Time every `every`-th stencil launch with HIP events (0/False = off)."""

@@ -242,9 +242,19 @@ struct gol_engine {
         std::vector<int64_t> pairs;
         int64_t* dpairs = nullptr;
         SegDesc* dev = nullptr;
+        // a copy of an earlier plan of the same rows (rank engines: the full-depth
+        // launches of a round share one plan); its device tables are the owner's
+        bool alias = false;
+        // autotuner: the candidate that runs (0 = the models' plan, else 1 + the
+        // index in tune_variant_names) and its best create-time launch vs the
+        // models' plan (ms; 0 = not tuned)
+        int32_t tuned = 0;
+        float tune_ms = 0.f, tune_ms_model = 0.f;
     };
     std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: see RankGeom
+    std::vector<int> plan_alias;  // plans[i] copies plans[plan_alias[i]] (-1: own plan)
     std::vector<std::vector<Plan>> plan_alts;  // autotuner candidates per plan (build_plans)
+    std::vector<std::vector<int32_t>> plan_alt_kind;  // each candidate's variant (1 + index)
 
     // row-block hand-off buffers (life_stencil.h): region 0 serves launches on
     // `stream`, region 1 those on `band_stream` (the two may run concurrently)
@@ -653,8 +663,15 @@ bool single_stream_skews(uint64_t h, uint64_t w, const gol_config* cfg)
     return false;
 }
 
+// Autotuner variants of a full-depth plan (build_plans, autotune_plans), in the
+// order build_plans makes them; gol_plan_tuning reports 1 + the index.
+constexpr int kTuneVariants = 4;
+constexpr const char* kTuneVariantNames[kTuneVariants] = {"no_half_strip", "skew_0.95",
+                                                          "skew_1.05", "other_block_kind"};
+
 void free_plan(gol_engine::Plan& q)
 {
+    if (q.alias) return;  // the owner's tables
     if (q.dev) (void)hipFree(q.dev);
     if (q.dpairs) (void)hipFree(q.dpairs);
     q.dev = nullptr;
@@ -894,28 +911,70 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                a.rows_young == b.rows_young && a.groups == b.groups &&
                a.pair_units == b.pair_units && a.segs[0].nblk == b.segs[0].nblk;
     };
+    // GOL_DEV_PLAN_VARIANT=<name> (tests/test_gpu_autotune.py): every full-depth plan
+    // that has the named autotuner variant runs it instead of the models' plan,
+    // without timing -- so each plan kind the autotuner can pick is pinned against
+    // the oracle at the shapes where it appears.
+    int forced = 0;
+    if (const char* fv = std::getenv("GOL_DEV_PLAN_VARIANT")) {
+        for (int i = 0; i < kTuneVariants; ++i)
+            if (std::strcmp(fv, kTuneVariantNames[i]) == 0) forced = i + 1;
+        if (!forced) return fail(GOL_EINVAL, std::string("GOL_DEV_PLAN_VARIANT: unknown variant ") + fv);
+    }
     e->plan_alts.assign(raw.size(), {});
+    e->plan_alt_kind.assign(raw.size(), {});
+    e->plan_alias.assign(raw.size(), -1);
     for (size_t pi = 0; pi < raw.size(); ++pi) {
+        // rows already planned (rank engines: the full-depth launches of a round
+        // share one region, rank_geometry): the same plan, resolved after the
+        // autotuner (resolve_aliases)
+        const bool role = e->overlap && pi >= (size_t)e->Hx;  // band / interior
+        for (size_t pj = 0; pj < pi && !role; ++pj) {
+            if (e->plan_alias[pj] >= 0 || raw[pj].size() != raw[pi].size()) continue;
+            bool same = true;
+            for (size_t k = 0; k < raw[pi].size() && same; ++k)
+                same = std::memcmp(&raw[pi][k], &raw[pj][k], sizeof(SegDesc)) == 0;
+            if (same) {
+                e->plan_alias[pi] = (int)pj;
+                break;
+            }
+        }
+        if (e->plan_alias[pi] >= 0) {
+            gol_engine::Plan a = e->plans[(size_t)e->plan_alias[pi]];
+            a.alias = true;
+            e->plans.push_back(a);
+            continue;
+        }
         gol_engine::Plan p;
         GOL_TRY(build_one(pi, hs, 1.0, handoff, p));
         e->plans.push_back(p);
         const bool full = e->nranks > 1 ? (pi < (size_t)e->Hx && (pi + 1) % e->K == 0) : pi == 0;
-        if (!tune || !full || p.segs.size() != 1 || p.lane_shift != 0 || !p.rows_old) continue;
+        if ((!tune && !forced) || !full || p.segs.size() != 1 || p.lane_shift != 0 || !p.rows_old)
+            continue;
         struct Variant {
             int64_t hs;
             double rho;
             uint32_t kind;
         };
+        // kTuneVariantNames order
         std::vector<Variant> vs = {{0, 1.0, handoff}, {hs, 0.95, handoff}, {hs, 1.05, handoff}};
         if (e->handoff == 0 && gol::handoff_kernel_exists((int)e->K, e->rule))
             vs.push_back({hs, 1.0, p.hand ? 1u : 2u});
-        for (const Variant& v : vs) {
+        for (size_t vi = 0; vi < vs.size(); ++vi) {
+            if (forced && (int)vi + 1 != forced) continue;
+            const Variant& v = vs[vi];
             gol_engine::Plan q;
             GOL_TRY(build_one(pi, v.hs, v.rho, v.kind, q));
             bool dup = q.segs.size() != 1 || same_plan(q, p);
             for (const auto& o : e->plan_alts[pi]) dup = dup || same_plan(q, o);
             if (dup) {
                 free_plan(q);
+                continue;
+            }
+            q.tuned = (int32_t)vi + 1;
+            if (forced) {  // the named variant replaces the models' plan
+                free_plan(e->plans[pi]);
+                e->plans[pi] = q;
                 continue;
             }
             e->plan_alts[pi].push_back(q);
@@ -1003,14 +1062,28 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     const int64_t glob0 = (int64_t)g->row0 - (int64_t)g->Hx;
     const int64_t in_field_lo = std::max<int64_t>(0, -glob0);
     const int64_t in_field_hi = std::min<int64_t>((int64_t)g->buf_rows, (int64_t)h - glob0);
+    // One region for the full-depth launches of a round (r04).  Launch j of a
+    // round (cumulative shrink c = jK; round_ops issues every full-depth launch
+    // before any shorter one) only needs the rows still valid, [c, buf - c), but
+    // it computes the first launch's rows [K, buf - K): the extra rows are
+    // computed from rows that are no longer valid, and no valid row ever reads
+    // them (row r after c generations needs rows [r - c, r + c] of the round's
+    // start).  Every full-depth launch then runs one block plan: the RCCL
+    // per-rank proxy's 4-way launches ran 148.7-155.0 us with the 8 shrinking
+    // plans of a round and 141.5 us with one plan repeated
+    // (profiles/r03/rocprof_kernel_stats_rank4_*.csv).  GOL_DEV_RANK_SHRINK=1
+    // restores the shrinking regions (dev A/B).
+    const char* shrink_v = std::getenv("GOL_DEV_RANK_SHRINK");
+    const bool shared = !(shrink_v && shrink_v[0] == '1');
     for (uint64_t c = 1; c <= g->Hx; ++c) {
+        const uint64_t cr = (shared && c % g->K == 0) ? g->K : c;
         SegDesc s{};
         s.base_row = 0;
         s.in_rows = (int64_t)g->buf_rows;
         s.glob0 = glob0;
         s.field_h = (int64_t)h;
-        s.out_lo = std::max<int64_t>((int64_t)c, in_field_lo);
-        s.out_hi = std::min<int64_t>((int64_t)(g->buf_rows - c), in_field_hi);
+        s.out_lo = std::max<int64_t>((int64_t)cr, in_field_lo);
+        s.out_hi = std::min<int64_t>((int64_t)(g->buf_rows - cr), in_field_hi);
         g->raw.push_back({s});
     }
     // overlap plans: rows neighbours need = own rows [Hx, 2Hx) (to rank-1) and
@@ -1117,6 +1190,7 @@ void step_schedule(uint32_t K, uint64_t Hx, bool overlap, bool halo_fresh, uint6
 
 gol_status plan_resident(gol_engine* e, const gol_config* cfg);
 gol_status autotune_plans(gol_engine* e);
+void resolve_aliases(gol_engine* e);
 
 // Kernels that wait for other wavefronts of their own launch -- hand-off row blocks
 // (life_stencil.h) and the resident kernel -- need every wavefront they wait for
@@ -1264,7 +1338,9 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
     gol_status st = GOL_OK;
     {
         // plan and register under the lock, so that engines created by several
-        // threads see each other (wait_release)
+        // threads see each other (wait_release).  The registry entry covers every
+        // candidate the autotuner may pick; the timing itself runs after the lock
+        // is released (it takes tens of ms), and the entry is narrowed to the pick.
         std::lock_guard<std::mutex> lock(g_wait_mu);
         const bool off = wait_registry_off();
         const WaitReg reg = g_wait_reg[e->device];
@@ -1273,7 +1349,6 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         if (!off && reg.hand) c.resident = 1;
         st = build_plans(e, raw);
         if (st == GOL_OK) st = plan_resident(e, &c);
-        if (st == GOL_OK) st = autotune_plans(e);
         if (st == GOL_OK && !off) {
             WaitReg& r = g_wait_reg[e->device];
             if (e->res.on) {
@@ -1282,6 +1357,8 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
             } else {
                 bool hand = false;
                 for (const auto& pl : e->plans) hand |= pl.hand && pl.multi_blk;
+                for (const auto& alts : e->plan_alts)
+                    for (const auto& pl : alts) hand |= pl.hand && pl.multi_blk;
                 if (hand && e->side[0]) {
                     e->reg_hand = true;
                     r.hand = e;
@@ -1289,7 +1366,19 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
             }
         }
     }
+    if (st == GOL_OK) st = autotune_plans(e);
     if (st != GOL_OK) return st;
+    resolve_aliases(e);
+    if (e->reg_hand) {
+        bool hand = false;
+        for (const auto& pl : e->plans) hand |= pl.hand && pl.multi_blk;
+        if (!hand) {  // the autotuner picked classic blocks: free the device's entry
+            std::lock_guard<std::mutex> lock(g_wait_mu);
+            WaitReg& r = g_wait_reg[e->device];
+            if (r.hand == e) r.hand = nullptr;
+            e->reg_hand = false;
+        }
+    }
     HIP_TRY(hipStreamSynchronize(e->stream));
     return GOL_OK;
 }
@@ -1608,6 +1697,8 @@ gol_status autotune_plans(gol_engine* e)
         for (size_t c = 1; c < cand.size(); ++c)
             if (best[c] < best[pick] && best[c] < kTuneMargin * best[0]) pick = c;
         e->plans[pi] = cand[pick];
+        e->plans[pi].tune_ms = best[pick];
+        e->plans[pi].tune_ms_model = best[0];
         for (size_t c = 0; c < cand.size(); ++c)
             if (c != pick) free_plan(cand[c]);
         if (std::getenv("GOL_DEV_PLANS"))
@@ -1621,6 +1712,17 @@ gol_status autotune_plans(gol_engine* e)
     (void)hipEventDestroy(t1);
     if (st == GOL_OK) st = check_err(e);  // a hand-off wait that timed out is a failure here too
     return st;
+}
+
+// Plans that share rows with an earlier plan (build_plans) become copies of it as
+// the autotuner left it: one block plan for every full-depth launch of a round.
+void resolve_aliases(gol_engine* e)
+{
+    for (size_t pi = 0; pi < e->plans.size() && pi < e->plan_alias.size(); ++pi)
+        if (e->plan_alias[pi] >= 0) {
+            e->plans[pi] = e->plans[(size_t)e->plan_alias[pi]];
+            e->plans[pi].alias = true;
+        }
 }
 
 // Order everything the side streams of a stripe engine have enqueued (band
@@ -2078,15 +2180,9 @@ void gol_destroy(gol_engine* e)
         if (ev) (void)hipEventDestroy(ev);
     if (e->band_stream) (void)hipStreamDestroy(e->band_stream);
     if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
-    for (auto& p : e->plans) {
-        if (p.dev) (void)hipFree(p.dev);
-        if (p.dpairs) (void)hipFree(p.dpairs);
-    }
+    for (auto& p : e->plans) free_plan(p);
     for (auto& alts : e->plan_alts)
-        for (auto& p : alts) {
-            if (p.dev) (void)hipFree(p.dev);
-            if (p.dpairs) (void)hipFree(p.dpairs);
-        }
+        for (auto& p : alts) free_plan(p);
     for (int b = 0; b < 2; ++b) {
         if (e->alloc[b]) (void)hipFree(e->alloc[b]);
         if (e->side[b]) (void)hipFree(e->side[b]);
@@ -2614,6 +2710,76 @@ gol_status gol_digest(gol_engine* e, uint64_t* live, uint64_t* hash)
     *live = acc[0];
     *hash = acc[1];
     return check_err(e);
+}
+
+gol_status gol_digest_rows(gol_engine* e, uint64_t row0, uint64_t rows, uint64_t* live,
+                           uint64_t* hash)
+{
+    if (!e || !live || !hash) return fail(GOL_EINVAL, "null argument");
+    if (row0 > e->H || rows > e->H - row0) return fail(GOL_EINVAL, "rows outside the field");
+    if (!e->parts.empty()) {
+        uint64_t L = 0, Hs = 0;
+        for (auto* p : e->parts) {
+            uint64_t l, h;
+            gol_status st = gol_digest_rows(p, row0, rows, &l, &h);
+            if (st != GOL_OK) return st;
+            L += l;
+            Hs += h;
+        }
+        *live = L;
+        *hash = Hs;
+        return GOL_OK;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    GOL_TRY(join_side_streams(e));
+    HIP_TRY(hipMemsetAsync(e->d_acc, 0, 2 * sizeof(unsigned long long), e->stream));
+    for (const auto& r : e->user_regions) {
+        // the field rows of this region inside [row0, row0 + rows)
+        const uint64_t lo = std::max<uint64_t>(r.glob_row, row0);
+        const uint64_t hi = std::min<uint64_t>(r.glob_row + r.rows, row0 + rows);
+        if (hi <= lo) continue;
+        HIP_TRY(gol::launch_digest(e->buf[e->cur], (int64_t)e->stride, (int64_t)e->wq,
+                                   (int64_t)e->ng, (int64_t)(r.buf_row + (lo - r.glob_row)),
+                                   (int64_t)lo, (int64_t)(hi - lo), e->d_acc, e->planes,
+                                   e->stream));
+    }
+    unsigned long long acc[2];
+    HIP_TRY(hipMemcpyAsync(acc, e->d_acc, sizeof(acc), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    *live = acc[0];
+    *hash = acc[1];
+    return check_err(e);
+}
+
+gol_status gol_comm_info(gol_engine* e, int* count, int* rank, int* peer_up, int* peer_down,
+                         int* device)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->comm) return fail(GOL_ESTATE, "engine has no RCCL communicator");
+    int n = 0, r = -1, d = -1;
+    NCCL_TRY(ncclCommCount(e->comm, &n));
+    NCCL_TRY(ncclCommUserRank(e->comm, &r));
+    NCCL_TRY(ncclCommCuDevice(e->comm, &d));
+    if (count) *count = n;
+    if (rank) *rank = r;
+    if (peer_up) *peer_up = e->rank > 0 ? e->peer_up : -1;
+    if (peer_down) *peer_down = e->rank < e->nranks - 1 ? e->peer_dn : -1;
+    if (device) *device = d;
+    return GOL_OK;
+}
+
+gol_status gol_plan_tuning(gol_engine* e, uint32_t* variant, float* tuned_us, float* model_us)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    if (!e->parts.empty()) return gol_plan_tuning(e->parts[0], variant, tuned_us, model_us);
+    if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
+    const bool rk = e->nranks > 1 && e->Hx >= e->K;
+    const auto& p = rk ? e->plans[e->K - 1] : e->plans[0];
+    const bool on = !e->res.on;
+    if (variant) *variant = on ? (uint32_t)p.tuned : 0u;
+    if (tuned_us) *tuned_us = on ? 1e3f * p.tune_ms : 0.f;
+    if (model_us) *model_us = on ? 1e3f * p.tune_ms_model : 0.f;
+    return GOL_OK;
 }
 
 gol_status gol_set_timing(gol_engine* e, int every)

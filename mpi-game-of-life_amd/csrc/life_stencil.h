@@ -59,6 +59,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <climits>
 #include <type_traits>
 
@@ -313,7 +314,7 @@ constexpr uint64_t kWaitTicks = 200000000ull;
 __device__ __forceinline__ uint64_t wait_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
 // Block modes of the stencil kernel (see `block`).
-constexpr int kWarmBlk = 0, kPure = 1, kSide = 2;
+constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 
 // Dev timing experiments only (tools/exp_build.sh; results are NOT valid): bit 0
 // skips the consumer's wait, bit 1 the producer's drain + flag, bit 2 the
@@ -524,17 +525,37 @@ void life_tb_kernel(StepArgs a)
     auto row_mask = [&](int32_t r) -> uint32_t {  // r: field row relative to glob0 + row_first
         return __builtin_amdgcn_readfirstlane((r >= f_lo) && (r < f_hi) ? ~0u : 0u);
     };
-    auto stage_rm = [&](int g, Pl<NP> x, uint32_t rm) -> Pl<NP> {
+    auto stage_rm = [&](int g, Pl<NP> x, uint32_t rm, auto masked) -> Pl<NP> {
         x = stage_step<RULE>(st[g], x, a.birth, a.survive);
-        if constexpr (kBirths) {
+        if constexpr (kBirths && decltype(masked)::value) {
 #pragma unroll
             for (int k = 0; k < NP; ++k) x.v[k] = lop3<kAnd3>(x.v[k], cm.v[k], rm);
         }
         return x;
     };
     auto stage = [&](int g, int32_t t, Pl<NP> x) -> Pl<NP> {
-        return stage_rm(g, x, kBirths ? row_mask(t - (g + 1)) : 0u);
+        return stage_rm(g, x, kBirths ? row_mask(t - (g + 1)) : 0u, std::true_type{});
     };
+    // Steady blocks without the births mask (r04).  The mask only changes cells the
+    // unit holds outside the field: lanes outside it or bits >= w of the last
+    // group (a per-lane column mask that is not all ones), and rows outside
+    // [0, field_h).  Rows above the field are emitted only in the warm-up (stage g
+    // emits row t - g - 1 at step t, and the first row of the field is at most K
+    // rows below the stream's first, f_lo <= K, so t < f_lo + K <= 2K <= warm-up),
+    // rows below it only by the last blocks of a stream that reaches past the
+    // field.  So a unit whose lanes are all inside the field runs its steady blocks
+    // up to the first that can emit row f_hi unmasked (kPure) and the rest masked
+    // (kPureMask); in a B3/S23 launch that is every unit but those of the field's
+    // last row blocks and of narrow or ragged columns (two v_bitop3 fewer per
+    // stage-step of 30.6 issue slots).
+    int32_t t_plain_end = INT32_MAX;  // steady blocks from t0 >= t_plain_end mask
+    if constexpr (kBirths) {
+        bool full = true;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) full = full && cm.v[k] == ~0u;
+        const bool lanes_in = __builtin_amdgcn_ballot_w64(!full) == 0;
+        t_plain_end = (lanes_in && f_lo + K <= kWarmSteps) ? f_hi - kPrefetch + 2 : INT32_MIN;
+    }
     auto store = [&](int32_t t, const Pl<NP>& x) {
         if (t >= 2 * K && t < T && st_lane)
             *reinterpret_cast<Grp<NP>*>(out_rows + (int64_t)(t - 2 * K) * row_bytes + voff) =
@@ -598,6 +619,8 @@ void life_tb_kernel(StepArgs a)
         constexpr int kMode = decltype(mode)::value;
         constexpr bool kGuard = kMode == kWarmBlk;
         constexpr bool kSideMode = HAND && kMode == kSide;
+        // births masked everywhere but in kPure blocks (t_plain_end)
+        constexpr bool kMask = kBirths && kMode != kPure;
         Pl<NP> x[kPrefetch];
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
@@ -619,7 +642,7 @@ void life_tb_kernel(StepArgs a)
         // the block's row masks, computed ahead of the compute (scalar code stays out
         // of the placed region): stage g at step t0 + p emits row t0 + p - g - 1
         uint32_t rmv[kPrefetch + K - 1];
-        if constexpr (kBirths) {
+        if constexpr (kMask) {
 #pragma unroll
             for (int j = 0; j < kPrefetch + K - 1; ++j) rmv[j] = row_mask(t0 - K + j);
         }
@@ -637,7 +660,8 @@ void life_tb_kernel(StepArgs a)
             for (int p = 0; p < kPrefetch; ++p) {
                 const int g = d - p;
                 if (g >= 0 && g < K && (!kGuard || t0 + p >= 2 * g)) {
-                    x[p] = stage_rm(g, x[p], kBirths ? rmv[p - g - 1 + K] : 0u);
+                    x[p] = stage_rm(g, x[p], kMask ? rmv[p - g - 1 + K] : 0u,
+                                    std::integral_constant<bool, kMask>{});
                     if constexpr (HAND && kGuard && !(GOL_EXP & 4)) {
                         if (g <= K - 2 && (t0 + p == 2 * g + 2 || t0 + p == 2 * g + 3))
                             store_side<NP>(reinterpret_cast<uint64_t*>(
@@ -694,11 +718,20 @@ void life_tb_kernel(StepArgs a)
     // refills reach the side rows) are peeled off the hot loop.
     int32_t t0 = kWarm;
     if constexpr (!HAND) {
-        for (; t0 < T; t0 += kPrefetch) block(t0, std::integral_constant<int, kPure>{});
+        for (; t0 < T && t0 < t_plain_end; t0 += kPrefetch)
+            block(t0, std::integral_constant<int, kPure>{});
+        if constexpr (kBirths)
+            for (; t0 < T; t0 += kPrefetch) block(t0, std::integral_constant<int, kPureMask>{});
     } else {
         // the consumer's wait is in the last pure block
-        for (; consumer ? t0 + 2 * kPrefetch + TOFF <= t_side : t0 < T; t0 += kPrefetch)
+        auto pure_more = [&](int32_t t) {
+            return consumer ? t + 2 * kPrefetch + TOFF <= t_side : t < T;
+        };
+        for (; pure_more(t0) && t0 < t_plain_end; t0 += kPrefetch)
             block(t0, std::integral_constant<int, kPure>{});
+        if constexpr (kBirths)
+            for (; pure_more(t0); t0 += kPrefetch)
+                block(t0, std::integral_constant<int, kPureMask>{});
         if (consumer)
             for (; t0 + kPrefetch + TOFF <= t_side; t0 += kPrefetch)
                 block(t0, std::integral_constant<int, kSide>{});
@@ -851,6 +884,23 @@ hipError_t launch_depth(const StepArgs& a, RuleKind rule, int planes, bool hand,
     return launch_planes<K, 2>(a, rule, hand, s);
 }
 
+// Blocks per CU of the hand-off kernels of one depth: the LEAST over every tail
+// offset that launch_planes can pick (their register use differs: offset 2 needs
+// 258 VGPRs and is capped), since a hand-off launch must fit in one round of
+// whichever offset its row lengths select (pick_rows_per_wave).
+template <int K, int NP>
+int occupancy_hand(RuleKind rule)
+{
+    constexpr int pf = kPfOf<NP, K>();
+    int occ = occupancy_kernel<K, NP, true, 0>(rule);
+    occ = std::min(occ, occupancy_kernel<K, NP, true, pf / 2>(rule));
+    if constexpr (pf == 8) {
+        occ = std::min(occ, occupancy_kernel<K, NP, true, (pf == 8 ? 2 : 0)>(rule));
+        occ = std::min(occ, occupancy_kernel<K, NP, true, (pf == 8 ? 6 : 0)>(rule));
+    }
+    return occ;
+}
+
 template <int K>
 int occupancy_depth(RuleKind rule, int planes, bool hand)
 {
@@ -858,13 +908,13 @@ int occupancy_depth(RuleKind rule, int planes, bool hand)
     if (planes == 4) {
         if constexpr (depth_has_planes(K, 4)) {
             if constexpr (K >= kHandoffMinDepth)
-                if (hand) return occupancy_kernel<K, 4, true, 0>(rule);
+                if (hand) return occupancy_hand<K, 4>(rule);
             return occupancy_kernel<K, 4, false, 0>(rule);
         }
         return 0;
     }
     if constexpr (K >= kHandoffMinDepth)
-        if (hand) return occupancy_kernel<K, 2, true, 0>(rule);
+        if (hand) return occupancy_hand<K, 2>(rule);
     return occupancy_kernel<K, 2, false, 0>(rule);
 }
 

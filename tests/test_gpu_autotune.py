@@ -86,3 +86,79 @@ def test_autotune_respects_waiting_kernel_registry(pkg, oracle, autotune):
     finally:
         a.close()
         b.close()
+
+
+# ---- every variant the autotuner can pick, forced (GOL_DEV_PLAN_VARIANT) ----
+# build_plans makes the named variant of every full-depth plan and runs it in
+# place of the models' plan, untimed.  A variant that equals the models' plan at
+# a shape is dropped there by the autotuner too (tuning reports "models").
+VARIANTS = ["no_half_strip", "skew_0.95", "skew_1.05", "other_block_kind"]
+_C3_WANT = {}
+
+
+def _c3_want(oracle, rule, gens):
+    """Oracle digest of the 65536^2 bench field after `gens` generations."""
+    key = (rule, gens)
+    if key not in _C3_WANT:
+        R = oracle.REF_RULE if rule == "ref" else oracle.CONWAY
+        g = oracle.bp_run(oracle.bp_random(W, W, 4), W, gens, R, threads=THREADS)
+        _C3_WANT[key] = oracle.bp_digest(g, W)
+    return _C3_WANT[key]
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_forced_variant_c3_vs_oracle(pkg, oracle, monkeypatch, variant, rule):
+    """65536^2 (the C3 headline field) with the variant forced: one K = 16 launch
+    and one more plus a remainder, against the oracle."""
+    monkeypatch.setenv("GOL_DEV_PLAN_VARIANT", variant)
+    R = pkg.REF_RULE if rule == "ref" else pkg.CONWAY
+    with pkg.Engine(W, W, rule=R, device=0) as e:
+        ran = e.tuning[0]
+        e.init_random(4)
+        e.step(16)
+        d16 = e.digest()
+        e.step(16 + 5)
+        d37 = e.digest()
+    assert ran in (variant, "models"), ran
+    assert d16 == _c3_want(oracle, rule, 16), f"{variant} ({ran}) after one launch"
+    assert d37 == _c3_want(oracle, rule, 37), f"{variant} ({ran}) after 37 generations"
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_forced_variant_rank8_vs_oracle(pkg, oracle, monkeypatch, variant, rule):
+    """The 8-way C4 rank shape (8192 own rows + 2 x 256 halo rows, its round's
+    full-depth launches sharing one plan) with the variant forced, over an RCCL
+    self-loop: against the oracle of the mirrored stripe (test_gpu_rccl.py)."""
+    from test_gpu_rccl import mirrored_steps
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    monkeypatch.setenv("GOL_DEV_PLAN_VARIANT", variant)
+    R = oracle.REF_RULE if rule == "ref" else oracle.CONWAY
+    n, world, rank, gens = 65536, 8, 3, 2 * 16 + 5
+    with pkg.Engine(n, n, rule=R, device=0, rank=rank, nranks=world,
+                    uid=pkg.unique_id()) as e:
+        ran, hx = e.tuning[0], e.halo_depth
+        e.init_random(3)
+        own = e.store_packed()
+        e.step(gens)
+        got = e.store_packed()
+    assert ran in (variant, "models"), ran
+    want = mirrored_steps(oracle, own, n, [gens], R, hx, True, True)[0]
+    assert (got == want).all(), f"{variant} ({ran})"
+
+
+def test_tuning_report(pkg, monkeypatch):
+    """gol_plan_tuning: the models' plan untimed with the autotuner off; a forced
+    variant is reported by name; an autotuned engine reports both timings."""
+    monkeypatch.setenv("GOL_DEV_AUTOTUNE", "0")
+    with pkg.Engine(W, W, device=0) as e:
+        assert e.tuning == ("models", 0.0, 0.0)
+    monkeypatch.setenv("GOL_DEV_PLAN_VARIANT", "no_half_strip")
+    with pkg.Engine(W, W, device=0) as e:
+        assert e.tuning[0] == "no_half_strip" and e.columns[1] == 0
+    monkeypatch.delenv("GOL_DEV_PLAN_VARIANT")
+    monkeypatch.setenv("GOL_DEV_AUTOTUNE", "1")
+    with pkg.Engine(W, W, device=0) as e:
+        v, t, m = e.tuning
+        assert v in pkg.TUNE_VARIANTS and t > 0 and m > 0 and t <= m

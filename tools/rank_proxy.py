@@ -84,6 +84,8 @@ def main():
                    "(0 auto = blocking for rank engines, 1 blocking, 2 overlapped)")
     p.add_argument("--transports", default="noop", help="noop and/or rccl (self-loop)")
     p.add_argument("--halo-depths", default="0", help="gol_config.halo_depth values (0 = auto)")
+    p.add_argument("--shrinks", default="0", help="GOL_DEV_RANK_SHRINK values: 0 = one region "
+                   "for the full-depth launches of a round (default), 1 = shrinking regions")
     a = p.parse_args()
     pkg = entry.load_package()
     n = a.size
@@ -94,6 +96,8 @@ def main():
         for trn in a.transports.split(","):
             for ov in (int(x) for x in a.overlaps.split(",")):
                 for hx in (int(x) for x in a.halo_depths.split(",")):
+                  for shr in a.shrinks.split(","):
+                    os.environ["GOL_DEV_RANK_SHRINK"] = shr
                     for sk in a.skews.split(","):
                         if sk == "auto":
                             os.environ.pop("GOL_DEV_AGE_SKEW", None)
@@ -103,8 +107,9 @@ def main():
                         e.init_random(1)
                         e.step(a.gens)
                         e.sync()
-                        engines.append(((sk, ov, trn), e, []))
+                        engines.append(((sk, ov, trn, shr), e, []))
         os.environ.pop("GOL_DEV_AGE_SKEW", None)
+        os.environ.pop("GOL_DEV_RANK_SHRINK", None)
         for _ in range(a.rounds):
             for sk, e, ts in engines:
                 t0 = time.perf_counter()
@@ -118,7 +123,8 @@ def main():
                               "halo_depth": e.halo_depth, "tb_depth": e.tb_depth,
                               "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
                               "age_skew": e.age_skew, "skew_cfg": sk[0], "overlap_cfg": sk[1],
-                              "transport": sk[2],
+                              "transport": sk[2], "shrink_cfg": sk[3],
+                              "autotune": list(e.tuning),
                               "rank_tcups": round(rate, 2),
                               "aggregate_tcups_if_balanced": round(rate * N, 1),
                               "ms_per_1000_gens": round(t * 1e3 * 1000 / a.gens, 2)}), flush=True)
