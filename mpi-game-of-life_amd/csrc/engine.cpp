@@ -63,13 +63,19 @@ Layout auto_layout(uint64_t rows, const gol_config* cfg)
                        (cfg->birth_mask == GOL_CONWAY_BIRTH &&
                         cfg->survive_mask == GOL_CONWAY_SURVIVE);
     Layout l;
-    if (cfg->tb_depth)
+    l.planes = cfg->word_planes ? (int)cfg->word_planes : 2;
+    // resident = 2 takes any epoch length; the streaming launches of an engine
+    // that cannot run the resident kernel (rank engines, composite parts, fields
+    // it does not fit) then use the auto depth when that length has no stencil
+    // kernel, instead of failing
+    const bool res_only = cfg->resident == 2 && cfg->tb_depth &&
+                          !gol::life_has_kernel((int)cfg->tb_depth, l.planes);
+    if (cfg->tb_depth && !res_only)
         l.K = cfg->tb_depth;
     else if (cfg->word_planes == 4 || rows <= 6144)
         l.K = 8;
     else
         l.K = fixed ? 16 : 12;
-    l.planes = cfg->word_planes ? (int)cfg->word_planes : 2;
     return l;
 }
 
@@ -1247,9 +1253,6 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->rule = gol::RULE_GENERIC;
     const Layout lay = auto_layout(e->R, cfg);
     e->K = lay.K;
-    // a resident epoch length with no streaming kernel of that depth: the
-    // streaming plans (never launched while the resident kernel runs) use 16
-    if (cfg->resident == 2 && !gol::life_has_kernel((int)e->K, lay.planes)) e->K = 16;
     e->rows_per_wave = cfg->rows_per_wave;
     e->lane_shift = cfg->strip_lanes == 64 ? 0 : cfg->strip_lanes == 32 ? 1
                   : cfg->strip_lanes == 16 ? 2 : -1;
@@ -2008,6 +2011,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     // lists exactly the launches gol_step runs
     gol_config c = *cfg;
     c.resident = 1;
+    c.tb_depth = g.K;  // (a resident-only epoch length maps to the auto depth)
     st = init_common(e, h, w, &c, &g);
     if (st != GOL_OK) {
         std::string msg = g_last_error;

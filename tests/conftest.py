@@ -9,11 +9,11 @@ if ROOT not in sys.path:
 
 import __graft_entry__ as entry  # noqa: E402
 
-# Plans as the cost models choose them: the engine's autotuner (engine.cpp
-# autotune_plans) times variants at create and may pick another, equally exact
-# one; tests that pin plan properties need the models' choice.  The autotuner
-# itself is covered in test_gpu_autotune.py.
-os.environ.setdefault("GOL_DEV_AUTOTUNE", "0")
+# The engine's autotuner (engine.cpp autotune_plans) times a few variants of the
+# cost models' plan at create and may pick another, equally exact one.  Parity
+# tests run with it on (the shipped default); tests that pin plan properties (the
+# skew lengths, the half strip's layout, the waiting-kernel registry's block
+# kinds) take the `model_plans` fixture.  test_gpu_autotune.py forces each variant.
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
@@ -21,6 +21,12 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libgol.so on the GPU)")
     config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture
+def model_plans(monkeypatch):
+    """The cost models' plans (GOL_DEV_AUTOTUNE=0) for tests that assert them."""
+    monkeypatch.setenv("GOL_DEV_AUTOTUNE", "0")
 
 
 @pytest.fixture(scope="session")

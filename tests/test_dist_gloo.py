@@ -235,3 +235,15 @@ def test_gol_mpi_dry_run_partition(pkg, tmp_path):
                           "--transport", "carrier-pigeon"], capture_output=True, text=True,
                          timeout=120)
     assert bad.returncode != 0
+
+
+def test_resident_epoch_length_maps_to_streaming_depth(pkg):
+    """resident = 2 takes any epoch length (tb_depth 1..63); a rank engine runs
+    the streaming kernel, whose depth is then the auto one when that length has no
+    stencil kernel (22 -> 16 at the 8-way 65536^2 stripe, 8 for short stripes)."""
+    _, K, Hx = pkg.round_schedule(65536, 65536, 1, 8, 100, resident=2, tb_depth=22)
+    assert (K, Hx) == (16, 256)
+    _, K, _ = pkg.round_schedule(4096, 4096, 0, 2, 40, resident=2, tb_depth=22)
+    assert K == 8
+    _, K, _ = pkg.round_schedule(4096, 4096, 0, 2, 40, resident=2, tb_depth=12)
+    assert K == 12

@@ -13,7 +13,8 @@ half strip (GOL_DEV_PAIRS=0).
 """
 import pytest
 
-pytestmark = pytest.mark.gpu
+# plan properties: the cost models' plans (conftest.py model_plans)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("model_plans")]
 
 THREADS = 16
 

@@ -196,7 +196,7 @@ def test_one_waiting_launch_per_device(pkg, oracle):
     assert (got == oracle.bp_run(g, w, 300, oracle.CONWAY, threads=16)).all()
 
 
-def test_waiting_kernel_registry_two_default_engines(pkg, oracle):
+def test_waiting_kernel_registry_two_default_engines(pkg, oracle, model_plans):
     """Two default engines of one process on one GPU at a hand-off shape (8448 x
     65536: one-round launches with hand-off blocks when alone), stepped without
     syncs in between: only the first keeps hand-off blocks (engine.cpp wait

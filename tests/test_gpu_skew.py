@@ -10,7 +10,8 @@ the same engine with equal blocks.
 """
 import pytest
 
-pytestmark = pytest.mark.gpu
+# plan properties: the cost models' plans (conftest.py model_plans)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("model_plans")]
 
 W = 65536
 THREADS = 16
