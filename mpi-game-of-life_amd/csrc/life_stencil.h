@@ -71,15 +71,33 @@ namespace gol {
 
 namespace {
 
+// GOL_XLANE_LDS (dev A/B, tools/variant_build.sh): the lane shifts through the
+// LDS crossbar (ds_bpermute_b32, no VALU issue slot) plus one full-rate AND for
+// the zero fill, instead of the half-rate DPP move.
+#ifndef GOL_XLANE_LDS
+#define GOL_XLANE_LDS 0
+#endif
 __device__ __forceinline__ uint32_t lane_from_left(uint32_t v)
 {
+#if GOL_XLANE_LDS
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 63) & 63) << 2, (int)v);
+    return r & (lane == 0 ? 0u : ~0u);
+#else
     // DPP wave_shr:1 -- lane l receives lane l-1's value; lane 0 receives 0.
     return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, true);
+#endif
 }
 __device__ __forceinline__ uint32_t lane_from_right(uint32_t v)
 {
+#if GOL_XLANE_LDS
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) << 2, (int)v);
+    return r & (lane == 63 ? 0u : ~0u);
+#else
     // DPP wave_shl:1 -- lane l receives lane l+1's value; lane 63 receives 0.
     return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xf, 0xf, true);
+#endif
 }
 
 // The NP 32-bit cell planes of one lane group (bitlayout.h): NP/2 words, 32*NP

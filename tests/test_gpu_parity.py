@@ -377,3 +377,43 @@ def test_graph_replay_matches(pkg, oracle):
             e.step(gens)
             total += gens
             assert (e.store_packed() == oracle.bp_run(g, w, total, oracle.CONWAY)).all(), total
+
+
+@pytest.mark.parametrize("h,w,kw", [
+    (1000, 777, {}),                         # resident kernel
+    (3000, 5000, dict(resident=1)),          # streaming kernel
+    (40000, 1000, dict(streams=2)),          # composite engine: 2 stripes
+])
+def test_digest_rows_partitions(pkg, oracle, h, w, kw):
+    """gol_digest_rows: the digests of a partition of the rows add up to the whole
+    field's (the order-independent sums of digest_kernel), the whole range is
+    gol_digest, and an empty range is (0, 0)."""
+    with pkg.Engine(h, w, rule=pkg.CONWAY, device=0, **kw) as e:
+        e.init_random(11)
+        e.step(19)
+        whole = e.digest()
+        assert e.digest_rows(0, h) == whole
+        assert e.digest_rows(5, 0) == (0, 0)
+        cuts = [0, 1, h // 3, h // 3 + 17, h - 1, h]
+        parts = [e.digest_rows(a, b - a) for a, b in zip(cuts, cuts[1:])]
+    assert sum(p[0] for p in parts) == whole[0]
+    assert sum(p[1] for p in parts) % (1 << 64) == whole[1]
+    want = oracle.bp_digest(oracle.bp_run(oracle.bp_random(h, w, 11), w, 19, oracle.CONWAY), w)
+    assert whole == want
+
+
+def test_digest_rows_rank_engine(pkg, monkeypatch):
+    """A rank engine's gol_digest_rows covers the part of its own rows inside the
+    range; the RCCL communicator as RCCL reports it (self-loop: 1 rank)."""
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    with pkg.Engine(1200, 640, rule=pkg.CONWAY, device=0, rank=1, nranks=3,
+                    uid=pkg.unique_id()) as e:
+        e.init_random(2)
+        e.step(30)
+        d = e.digest()
+        assert e.digest_rows(e.row0, e.rows) == d
+        assert e.digest_rows(0, 1200) == d
+        assert e.digest_rows(0, e.row0) == (0, 0)
+        ci = e.comm_info()
+    assert ci["count"] == 1 and ci["rank"] == 0 and ci["device"] == 0
+    assert ci["peer_up"] == 0 and ci["peer_down"] == 0  # the self-loop's peers
