@@ -1046,14 +1046,25 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     const uint64_t minR = h / (uint64_t)nranks;
     if (minR == 0) return fail(GOL_EINVAL, "fewer rows than ranks");
     g->K = auto_layout(g->R, cfg).K;
-    // Rounds of halo_depth generations between exchanges: 8 launches, or 16 for
-    // K = 16 stripes of at most 12288 rows.  Per-rank proxy over the RCCL byte mover
+    // Rounds of halo_depth generations between exchanges: 8 launches (r03, with
+    // shrinking regions: 16 for K = 16 stripes of at most 12288 rows).  Per-rank
+    // proxy over the RCCL byte mover
     // (self-loop communicator, tools/rank_proxy.py, profiles/r03/rank_proxy_rccl.jsonl):
     // the 8-way 65536^2 rank (8192 rows) ran 107.8 TCUPS at Hx = 128 and 109.3 at
     // 256 -- half the rounds, each with an exchange and a launch sequence whose
     // first, longest launch fits the one-round plans worst -- against 1.6% more halo
     // rows; the 4-way rank was 117.2 at 128 and 116.5-116.7 at 192-256.
-    const uint64_t launches_per_round = (g->K >= 16 && g->R <= 12288) ? 16 : 8;
+    //
+    // r04: with one region for the round's full-depth launches (below), each launch
+    // computes R + 2 Hx - 2K rows, so deeper halos cost rows on every launch, and
+    // 8 launches per round is best at every split (RCCL per-rank proxy, TCUPS of own
+    // rows, Hx = 128 vs 256: 8-way 110.0 vs 107.9, 4-way 120.9 vs 120.4;
+    // profiles/r04/rank_proxy_rccl_halo_depth.jsonl).  The shrinking regions
+    // (GOL_DEV_RANK_SHRINK=1) keep the r03 depths.
+    const char* shrink_env = std::getenv("GOL_DEV_RANK_SHRINK");
+    const bool shrinking = shrink_env && shrink_env[0] == '1';
+    const uint64_t launches_per_round =
+        (shrinking && g->K >= 16 && g->R <= 12288) ? 16 : 8;
     uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : launches_per_round * (uint64_t)g->K;
     if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
     g->Hx = nranks > 1 ? Hx : 0;
@@ -1079,8 +1090,7 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // plans of a round and 141.5 us with one plan repeated
     // (profiles/r03/rocprof_kernel_stats_rank4_*.csv).  GOL_DEV_RANK_SHRINK=1
     // restores the shrinking regions (dev A/B).
-    const char* shrink_v = std::getenv("GOL_DEV_RANK_SHRINK");
-    const bool shared = !(shrink_v && shrink_v[0] == '1');
+    const bool shared = !shrinking;
     for (uint64_t c = 1; c <= g->Hx; ++c) {
         const uint64_t cr = (shared && c % g->K == 0) ? g->K : c;
         SegDesc s{};

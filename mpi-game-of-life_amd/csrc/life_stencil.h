@@ -573,6 +573,9 @@ void life_tb_kernel(StepArgs a)
         for (int k = 0; k < NP; ++k) full = full && cm.v[k] == ~0u;
         const bool lanes_in = __builtin_amdgcn_ballot_w64(!full) == 0;
         t_plain_end = (lanes_in && f_lo + K <= kWarmSteps) ? f_hi - kPrefetch + 2 : INT32_MIN;
+#if defined(GOL_DEV_MASK_MODE) && GOL_DEV_MASK_MODE == 1
+        t_plain_end = INT32_MIN;  // dev A/B: every steady block masked (r03 behaviour)
+#endif
     }
     auto store = [&](int32_t t, const Pl<NP>& x) {
         if (t >= 2 * K && t < T && st_lane)
@@ -666,7 +669,7 @@ void life_tb_kernel(StepArgs a)
         }
         if constexpr (!kGuard) {
             __builtin_amdgcn_sched_barrier(0);
-            place_block<life_loop_pad(K, RULE, NP, HAND, TOFF) != 0, NP, kPrefetch>(x);
+            place_block<life_loop_pad(K, RULE, NP, HAND, TOFF, kMask ? 1 : 0) != 0, NP, kPrefetch>(x);
             __builtin_amdgcn_sched_barrier(0);
         }
         // stage g of step p only needs stage g-1 of step p and stage g of step
@@ -738,8 +741,10 @@ void life_tb_kernel(StepArgs a)
     if constexpr (!HAND) {
         for (; t0 < T && t0 < t_plain_end; t0 += kPrefetch)
             block(t0, std::integral_constant<int, kPure>{});
+#if !(defined(GOL_DEV_MASK_MODE) && GOL_DEV_MASK_MODE == 2)  // 2: timing only, no masked loop
         if constexpr (kBirths)
             for (; t0 < T; t0 += kPrefetch) block(t0, std::integral_constant<int, kPureMask>{});
+#endif
     } else {
         // the consumer's wait is in the last pure block
         auto pure_more = [&](int32_t t) {

@@ -162,12 +162,19 @@ def test_rank_protocol_from_engine_schedule(oracle, monkeypatch, world, K, Hx, c
     assert (got == ref_cells).all()
 
 
-def test_default_halo_depth(pkg):
-    """Rounds of 8 launches, 16 for K = 16 stripes of at most 12288 rows (the 8-way
-    65536^2 rank: engine.cpp rank_geometry)."""
+def test_default_halo_depth(pkg, monkeypatch):
+    """Rounds of 8 launches (engine.cpp rank_geometry: the round's full-depth
+    launches share one region, so deeper halos cost rows on every launch); with the
+    r03 shrinking regions (GOL_DEV_RANK_SHRINK=1) 16 for K = 16 stripes of at most
+    12288 rows (the 8-way 65536^2 rank)."""
+    for nranks, want in ((2, 128), (4, 128), (8, 128)):
+        _, K, Hx = pkg.round_schedule(65536, 65536, 1, nranks, 16)
+        assert (K, Hx) == (16, want), nranks
+    monkeypatch.setenv("GOL_DEV_RANK_SHRINK", "1")
     for nranks, want in ((2, 128), (4, 128), (8, 256)):
         _, K, Hx = pkg.round_schedule(65536, 65536, 1, nranks, 16)
         assert (K, Hx) == (16, want), nranks
+    monkeypatch.delenv("GOL_DEV_RANK_SHRINK")
     _, K, Hx = pkg.round_schedule(1200, 2000, 0, 2, 16, tb_depth=8)
     assert (K, Hx) == (8, 64)
 
@@ -242,7 +249,7 @@ def test_resident_epoch_length_maps_to_streaming_depth(pkg):
     the streaming kernel, whose depth is then the auto one when that length has no
     stencil kernel (22 -> 16 at the 8-way 65536^2 stripe, 8 for short stripes)."""
     _, K, Hx = pkg.round_schedule(65536, 65536, 1, 8, 100, resident=2, tb_depth=22)
-    assert (K, Hx) == (16, 256)
+    assert (K, Hx) == (16, 128)
     _, K, _ = pkg.round_schedule(4096, 4096, 0, 2, 40, resident=2, tb_depth=22)
     assert K == 8
     _, K, _ = pkg.round_schedule(4096, 4096, 0, 2, 40, resident=2, tb_depth=12)

@@ -49,9 +49,9 @@ def test_autotuned_equals_model_plans_c3(pkg, autotune, monkeypatch):
 
 
 def test_autotuned_rank_shape(pkg, monkeypatch):
-    """The 8-way C4 rank (8192 own rows + 2 x 256 halo rows, 16 full-depth plans
+    """The 8-way C4 rank (8192 own rows + 2 x 128 halo rows, one shared full-depth plan
     autotuned) over RCCL self-loops, against the models' plans (same field after
-    two rounds and a partial one)."""
+    four rounds and a partial one)."""
     monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
     n, world, rank, gens = 65536, 8, 3, 2 * 256 + 40
     out = []
@@ -128,7 +128,7 @@ def test_forced_variant_c3_vs_oracle(pkg, oracle, monkeypatch, variant, rule):
 @pytest.mark.parametrize("rule", ["ref", "conway"])
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_forced_variant_rank8_vs_oracle(pkg, oracle, monkeypatch, variant, rule):
-    """The 8-way C4 rank shape (8192 own rows + 2 x 256 halo rows, its round's
+    """The 8-way C4 rank shape (8192 own rows + 2 x 128 halo rows, its round's
     full-depth launches sharing one plan) with the variant forced, over an RCCL
     self-loop: against the oracle of the mirrored stripe (test_gpu_rccl.py)."""
     from test_gpu_rccl import mirrored_steps

@@ -99,8 +99,8 @@ def test_rccl_self_loop(pkg, oracle, monkeypatch, world, rank, K, Hx, rule, over
 
 
 def test_rccl_self_loop_c4_rank_shape(pkg, monkeypatch):
-    """The 8-way C4 per-rank shape (8192 own rows of 65536^2 + 2 x 256 halo rows,
-    default K = 16, age-skewed one-round launches, default block kind): 2 MiB
+    """The 8-way C4 per-rank shape (8192 own rows of 65536^2 + 2 x 128 halo rows,
+    default K = 16, age-skewed one-round launches, default block kind): 1 MiB
     messages through RCCL every round, bytewise equal to the host loopback."""
     monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
     n, world, rank, gens = 65536, 8, 3, 2 * 256 + 40
@@ -108,7 +108,7 @@ def test_rccl_self_loop_c4_rank_shape(pkg, monkeypatch):
     for mode in ("rccl", "host"):
         kw = dict(uid=pkg.unique_id()) if mode == "rccl" else dict(transport=lambda su, sd: (su, sd))
         with pkg.Engine(n, n, rule=pkg.CONWAY, device=0, rank=rank, nranks=world, **kw) as e:
-            assert e.halo_depth == 256
+            assert e.halo_depth == 128
             e.init_random(3)
             e.step(gens)
             out.append((e.digest(), e.store_packed()))

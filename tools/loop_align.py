@@ -78,8 +78,12 @@ def vgpr_counts(notes):
     return out
 
 
-def main_loop_fraction(body):
-    """Fraction of the main loop's 8-byte instructions at 4 mod 8."""
+def main_loop_fractions(body, births):
+    """[(mask, fraction of the loop's 8-byte instructions at 4 mod 8, count)] for the
+    steady-state loops: one for B/S2 kernels; for kernels with births (r04) the
+    loop without the births mask (mask 0: the smaller one) and the masked loop
+    (mask 1: the bigger ones, kPureMask and a hand-off consumer's kSide blocks),
+    which get their own pad."""
     base = int(body[0].split()[0], 16)
     ins = []
     for l in body:
@@ -97,52 +101,62 @@ def main_loop_fraction(body):
         if len(eight) >= 32:
             cands.append((lo, hi, eight))
     if not cands:
-        return None, 0
-    # the steady-state loop: of the innermost candidate loops, the one with the most
-    # compute (the control flow may wrap bigger loops around it)
+        return []
+    # the steady-state loops: innermost candidates with the most compute (the
+    # control flow may wrap bigger loops around them; a hand-off kernel's flag
+    # polls split its blocks into several backward branches of about one size)
     inner = [c for c in cands
              if not any(d is not c and c[0] <= d[0] and d[1] <= c[1] for d in cands)]
-    # B3/S23 and generic kernels have two steady loops (r04: without and with the
-    # births mask, life_stencil.h t_plain_end), the same pad for both: report the
-    # worse-placed of the loops within 15% of the biggest
     top = max(len(c[2]) for c in inner)
-    fr = [(sum(1 for a in e8 if a % 8 == 4) / len(e8), len(e8)) for _, _, e8 in inner
-          if len(e8) >= 0.85 * top]
-    frac = min(f for f, _ in fr) if all(f >= 0.5 for f, _ in fr) else max(f for f, _ in fr)
-    return frac, "+".join(str(n) for _, n in fr)
+    big = [c for c in inner if len(c[2]) >= 0.8 * top]
+    frac = lambda e8: sum(1 for a in e8 if a % 8 == 4) / len(e8)
+    if not births:
+        lo, hi, e8 = max(big, key=lambda c: len(c[2]))
+        return [(0, frac(e8), len(e8))]
+    small = min(len(c[2]) for c in big)
+    out = []
+    for mask, grp in ((0, [c for c in big if len(c[2]) <= 1.04 * small]),
+                      (1, [c for c in big if len(c[2]) > 1.04 * small])):
+        if grp:
+            fr = [frac(c[2]) for c in grp]
+            # the worst-placed copy, unless some copy has 4-byte code inside (~50%)
+            f = min(fr) if all(x >= 0.5 for x in fr) or all(x < 0.5 for x in fr) else min(fr)
+            out.append((mask, f, len(grp[0][2])))
+    return out
 
 
 def current_pads():
     pads = set()
     if os.path.exists(HEADER):
-        for m in re.finditer(r"\{(\d+), (\d+), (\d+), (\d+), (\d+)\}", open(HEADER).read()):
+        for m in re.finditer(r"\{(\d+), (\d+), (\d+), (\d+), (\d+), (\d+)\}", open(HEADER).read()):
             if m.group(1) != "0":
                 pads.add(tuple(int(x) for x in m.groups()))
     return pads
 
 
 def write_header(pads):
-    rows = "".join(f"    {{{k}, {r}, {n}, {h}, {t}}},\n" for k, r, n, h, t in sorted(pads))
+    rows = "".join(f"    {{{k}, {r}, {n}, {h}, {t}, {mk}}},\n" for k, r, n, h, t, mk in sorted(pads))
     open(HEADER, "w").write(f"""// loop_place.h -- GENERATED by tools/loop_align.py --update from the built
-// libgol.so; do not edit by hand.  life_loop_pad(K, RULE, NP, HAND, TOFF) = 1
+// libgol.so; do not edit by hand.  life_loop_pad(K, RULE, NP, HAND, TOFF, MASK) = 1
 // adds a 4-byte s_nop after the 8-byte alignment before the compute of each
-// steady-state block of life_tb_kernel<K, RULE, NP, HAND, TOFF> (see
-// life_stencil.h).
+// steady-state block of life_tb_kernel<K, RULE, NP, HAND, TOFF> without (MASK 0)
+// or with (MASK 1) the births mask (see life_stencil.h).
 #pragma once
 
 namespace gol {{
 
 struct LoopPad {{
-    int K, rule, np, hand, toff;
+    int K, rule, np, hand, toff, mask;
 }};
 constexpr LoopPad kLoopPads[] = {{
-{rows}    {{0, 0, 0, 0, 0}}  // end
+{rows}    {{0, 0, 0, 0, 0, 0}}  // end
 }};
 
-constexpr int life_loop_pad(int K, int RULE, int NP, bool HAND, int TOFF)
+constexpr int life_loop_pad(int K, int RULE, int NP, bool HAND, int TOFF, int MASK)
 {{
     for (const LoopPad& p : kLoopPads)
-        if (p.K == K && p.rule == RULE && p.np == NP && p.hand == (HAND ? 1 : 0) && p.toff == TOFF)
+        if (p.K == K && p.rule == RULE && p.np == NP && p.hand == (HAND ? 1 : 0) && p.toff == TOFF &&
+            p.mask == MASK)
             return 1;
     return 0;
 }}
@@ -167,21 +181,20 @@ def main():
             continue
         key = tuple(int(x) for x in m.groups())
         end = next(j for j in range(i + 1, len(lines)) if not lines[j].strip())
-        frac, n = main_loop_fraction(lines[i:end])
-        if frac is None:
-            continue
         # 2+ waves per SIMD when the kernel fits 256 registers (512 per SIMD lane)
         want4 = vgprs.get(key, 0) <= 256 if vgprs else key[0] < 20
-        good = frac if want4 else 1.0 - frac
-        hot = key[1] in (0, 1) and key[0] >= 8
-        ok = good >= 0.9
-        print(f"life_tb_kernel<{key[0]:2d}, {key[1]}, {key[2]}, {bool(key[3])}, {key[4]}> ({vgprs.get(key, '?')} regs): "
-              f"{n:>9} 8-byte instrs, "
-              f"{100 * good:3.0f}% at {'4' if want4 else '0'} mod 8, pad {int(key in pads)}"
-              f"{'' if ok else '  <- misplaced'}")
-        if good < 0.35:  # a clear miss; ~50% means 4-byte code inside the compute
-            new ^= {key}
-        bad += int(hot and not ok)
+        for mask, frac, n in main_loop_fractions(lines[i:end], key[1] != 0):
+            kmask = key + (mask,)
+            good = frac if want4 else 1.0 - frac
+            hot = key[1] in (0, 1) and key[0] >= 8
+            ok = good >= 0.9
+            print(f"life_tb_kernel<{key[0]:2d}, {key[1]}, {key[2]}, {bool(key[3])}, {key[4]}> "
+                  f"{'masked' if mask else 'plain '} ({vgprs.get(key, '?')} regs): {n:5d} 8-byte instrs, "
+                  f"{100 * good:3.0f}% at {'4' if want4 else '0'} mod 8, pad {int(kmask in pads)}"
+                  f"{'' if ok else '  <- misplaced'}")
+            if good < 0.35:  # a clear miss; ~50% means 4-byte code inside the compute
+                new ^= {kmask}
+            bad += int(hot and not ok)
     if update and new != pads:
         write_header(new)
         print(f"updated {HEADER}: {len(new)} padded kernels; rebuild")
