@@ -28,7 +28,7 @@ prints one JSON line.
     with the best measured rate beside it (profiles/r01/valu_rate.json, 1067 G/s:
     peak_measured, frac_vs_measured);
   * valu.issue_frac: ALL VALU instructions per launch (rocprofv3 SQ_INSTS_VALU
-    of this configuration, committed in profiles/r03/counters.json: warm-up,
+    of this configuration, committed in profiles/r0N/counters.json: warm-up,
     masks and halo work included) at the same peak;
   * hbm_equiv_frac: SURVEY §8(d)'s 0.25 B per cell-generation x GCUPS / 8 TB/s
     (> 1 is what temporal blocking buys); hbm_measured_frac: the measured HBM
@@ -101,14 +101,16 @@ def counters_for(cfg):
     record with the same field, rule, depth, streams, GPUs and block kind whose
     rows per wavefront is the same or within 2% (a plan a row or two different
     moves the counters by well under 1%)."""
-    rec = load_json("profiles/r03/counters.json") or load_json("profiles/r02/counters.json") or {}
+    recs = []
+    for rnd in ("r04", "r03", "r02"):  # newest first
+        recs += (load_json(f"profiles/{rnd}/counters.json") or {}).get("records", [])
     keys = ("size", "rule", "tb_depth", "streams", "n_gpus", "handoff")
     best = None
-    for r in rec.get("records", []):
+    for r in recs:
         if not all(r.get(k) == cfg.get(k) for k in keys):
             continue
         d = abs(r.get("rows_per_wave", 0) - cfg.get("rows_per_wave", 0))
-        if d <= 0.02 * max(1, cfg.get("rows_per_wave", 0)) and (best is None or d < best[0]):
+        if d <= 0.02 * max(1, cfg.get("rows_per_wave", 0)) and (best is None or d < best[0]):  # noqa: E501
             best = (d, r)
     return best[1] if best else None
 
