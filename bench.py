@@ -96,6 +96,16 @@ def valu_peak_rate():
     return max(r.get("v_bitop3_b32_at_0mod8_2waves", 0.0), r.get("v_xor_b32", 0.0), 9.0e8)
 
 
+def valu_mix_rate():
+    """Measured issue-slot rate per SIMD of the stage's own instruction mix (1 DPP
+    move, 1 v_alignbit, 6 v_bitop3 per chain = 10 slots per 8 instructions; 2 waves
+    per SIMD, placed at 4 mod 8 like the kernel's loop): the ceiling the steady loop
+    can reach with this mix."""
+    r = load_json("profiles/r01/valu_rate.json") or {}
+    v = r.get("mix_at_4mod8_2w")
+    return v * 10.0 / 8.0 if v else None
+
+
 def counters_for(cfg):
     """Per-launch PMC record (SQ_INSTS_VALU, HBM bytes) of this configuration: the
     record with the same field, rule, depth, streams, GPUs and block kind whose
@@ -488,6 +498,11 @@ def main():
                 "frac_vs_measured": round(valu_achieved / meas_slot_rate, 4),
                 "peak_measured_from": "profiles/r01/valu_rate.json (v_bitop3, 2 waves/SIMD, best "
                                       "code placement) x 1024 SIMDs",
+                # the stage's instruction mix in a microbenchmark at 2 waves/SIMD
+                "peak_mix_measured": (round(SIMDS * valu_mix_rate() / 1e9, 1)
+                                      if valu_mix_rate() else None),
+                "frac_vs_mix": (round(valu_achieved / (SIMDS * valu_mix_rate()), 4)
+                                if valu_mix_rate() else None),
                 "traffic": traffic,
                 "kernel": "life_res_kernel" if eng.resident else "life_tb_kernel",
                 "avg_launch_ms": round(avg_launch_ms, 4),
