@@ -1056,15 +1056,19 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // rows; the 4-way rank was 117.2 at 128 and 116.5-116.7 at 192-256.
     //
     // r04: with one region for the round's full-depth launches (below), each launch
-    // computes R + 2 Hx - 2K rows, so deeper halos cost rows on every launch, and
-    // 8 launches per round is best at every split (RCCL per-rank proxy, TCUPS of own
-    // rows, Hx = 128 vs 256: 8-way 110.0 vs 107.9, 4-way 120.9 vs 120.4;
-    // profiles/r04/rank_proxy_rccl_halo_depth.jsonl).  The shrinking regions
-    // (GOL_DEV_RANK_SHRINK=1) keep the r03 depths.
+    // computes R + 2 Hx - 2K rows, so deeper halos cost rows on every launch (RCCL
+    // per-rank proxy, TCUPS of own rows, Hx = 128 vs 256: 8-way 110.0 vs 107.9,
+    // 4-way 120.9 vs 120.4; profiles/r04/rank_proxy_rccl_halo_depth.jsonl).  The
+    // shrinking regions (GOL_DEV_RANK_SHRINK=1) keep the r03 depths.
     const char* shrink_env = std::getenv("GOL_DEV_RANK_SHRINK");
     const bool shrinking = shrink_env && shrink_env[0] == '1';
+    // Stripes of 16384+ rows take 12 launches per round (Hx = 192 at K = 16): 4-way
+    // 121.2-122.6 vs 118.3-121.2 TCUPS at 128, 2-way equal, both in one process
+    // (profiles/r04/rank_proxy_rccl_halo_depth_sweep.jsonl); the 8-way rank keeps 8
+    // (64 / 96 / 128 / 160: 106.2 / 108.3 / 109.6 / 107.9).
     const uint64_t launches_per_round =
-        (shrinking && g->K >= 16 && g->R <= 12288) ? 16 : 8;
+        shrinking ? ((g->K >= 16 && g->R <= 12288) ? 16 : 8)
+                  : ((g->K >= 16 && g->R >= 16384) ? 12 : 8);
     uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : launches_per_round * (uint64_t)g->K;
     if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
     g->Hx = nranks > 1 ? Hx : 0;

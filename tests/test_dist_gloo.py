@@ -163,11 +163,12 @@ def test_rank_protocol_from_engine_schedule(oracle, monkeypatch, world, K, Hx, c
 
 
 def test_default_halo_depth(pkg, monkeypatch):
-    """Rounds of 8 launches (engine.cpp rank_geometry: the round's full-depth
-    launches share one region, so deeper halos cost rows on every launch); with the
+    """Rounds of 8 launches, 12 for K = 16 stripes of 16384+ rows (engine.cpp
+    rank_geometry: the round's full-depth launches share one region, so deeper
+    halos cost rows on every launch); with the
     r03 shrinking regions (GOL_DEV_RANK_SHRINK=1) 16 for K = 16 stripes of at most
     12288 rows (the 8-way 65536^2 rank)."""
-    for nranks, want in ((2, 128), (4, 128), (8, 128)):
+    for nranks, want in ((2, 192), (4, 192), (8, 128)):
         _, K, Hx = pkg.round_schedule(65536, 65536, 1, nranks, 16)
         assert (K, Hx) == (16, want), nranks
     monkeypatch.setenv("GOL_DEV_RANK_SHRINK", "1")

@@ -51,9 +51,9 @@ def test_c3_default_engine_vs_oracle_and_depth1(pkg, oracle, rule, streams):
 @pytest.mark.parametrize("nranks", [2, 4, 8])
 def test_c4_stripes_equal_single_field(pkg, nranks):
     """C4 partition: 65536^2 in `nranks` row stripes (gol_rank_rows), default K and
-    halo depth (8K = 128), 3 rounds + a
+    halo depth (8K = 128 for the 8192-row stripes, 12K = 192 above), 3 rounds + a
     partial one, overlapped exchanges."""
-    hx = 128
+    hx = 128 if nranks == 8 else 192
     gens = 3 * hx + 40
     want = digest_of(pkg, N, N, pkg.CONWAY, gens, seed=4)
     with pkg.Group(N, N, nranks, rule=pkg.CONWAY) as grp:
