@@ -6,7 +6,7 @@
 #   bash tools/gpu_steps.sh OUT STEP [STEP ...]
 #
 # Steps (arguments after ':' are split on spaces):
-#   tests[:ARGS]        the -m gpu suite (ARGS: extra pytest args, e.g. -k rccl)
+#   tests[:FILES]       the -m gpu suite (FILES: test files instead of all of tests/)
 #   smoke               __graft_entry__.smoke()
 #   bench:NAME[:ARGS]   python bench.py ARGS -> NAME.json
 #   rehearse2:NAME[:ARGS]  bench.py --gpus 2 on ONE GPU with self-looped RCCL
@@ -31,8 +31,8 @@ for step in "$@"; do
   echo "== $kind $name $args"
   case $kind in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 \
-          --timeout-method thread $rest > "$OUT/gpu_tests.log" 2>&1
+      timeout -k 10 900 python -u -m pytest ${rest:-tests} -m gpu -v -rf --timeout 300 \
+          --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
       rc=$?
       grep -E "passed|failed" "$OUT/gpu_tests.log" | tail -2
       if [ $rc -ne 0 ]; then grep -E "^FAILED|^ERROR" "$OUT/gpu_tests.log" | head -20; exit $rc; fi ;;
