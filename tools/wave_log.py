@@ -75,7 +75,22 @@ def main():
         span = max(end[i], end[j]) - min(start[i], start[j])
         solo.append((second - first) / 100.0)
         lead_share.append((second - first) / span)
+    # per SIMD, the share of the launch span with 2, 1 and 0 of its waves running
+    # (the issue model: full rate needs both; r04)
+    span_all = float(end.max() - t0)
+    conc = collections.Counter()
+    for v in pairs.values():
+        ev = sorted([(int(start[i]), 1) for i in v] + [(int(end[i]), -1) for i in v])
+        cur, last = 0, int(t0)
+        for t, d in ev:
+            conc[min(cur, 2)] += t - last
+            cur += d
+            last = t
+        conc[0] += int(end.max()) - last
+    tot = sum(conc.values()) or 1
+    concurrency = {str(k): round(conc[k] / tot, 4) for k in (2, 1, 0)}
     rec = {
+        "simd_time_share_by_waves_running": concurrency,
         "tag": a.tag, "lib": os.path.basename(os.environ.get("GOL_LIB", "libgol.so")),
         "shape": f"{a.rows}x{a.width}", "tb_depth": e.tb_depth, "rows_per_wave": e.rows_per_wave,
         "handoff": e.handoff, "tcups_wall_median": round(tcups, 2),
