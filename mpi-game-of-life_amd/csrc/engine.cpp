@@ -252,7 +252,7 @@ struct gol_engine {
         // launches of a round share one plan); its device tables are the owner's
         bool alias = false;
         // autotuner: the candidate that runs (0 = the models' plan, else 1 + the
-        // index in tune_variant_names) and its best create-time launch vs the
+        // index in kTuneVariantNames) and its best create-time launch vs the
         // models' plan (ms; 0 = not tuned)
         int32_t tuned = 0;
         float tune_ms = 0.f, tune_ms_model = 0.f;
@@ -260,7 +260,6 @@ struct gol_engine {
     std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: see RankGeom
     std::vector<int> plan_alias;  // plans[i] copies plans[plan_alias[i]] (-1: own plan)
     std::vector<std::vector<Plan>> plan_alts;  // autotuner candidates per plan (build_plans)
-    std::vector<std::vector<int32_t>> plan_alt_kind;  // each candidate's variant (1 + index)
 
     // row-block hand-off buffers (life_stencil.h): region 0 serves launches on
     // `stream`, region 1 those on `band_stream` (the two may run concurrently)
@@ -928,7 +927,6 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         if (!forced) return fail(GOL_EINVAL, std::string("GOL_DEV_PLAN_VARIANT: unknown variant ") + fv);
     }
     e->plan_alts.assign(raw.size(), {});
-    e->plan_alt_kind.assign(raw.size(), {});
     e->plan_alias.assign(raw.size(), -1);
     for (size_t pi = 0; pi < raw.size(); ++pi) {
         // rows already planned (rank engines: the full-depth launches of a round
