@@ -1660,9 +1660,9 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
 }
 
 // Autotuner (candidates from build_plans): each full-depth plan and its variants
-// run interleaved on the engine's buffers, 1 + 5 launches each timed with HIP
-// events (the stencil's time does not depend on the cells); the fastest by its
-// best launch replaces the models' plan if it is at least 3% faster (timings at
+// run interleaved on the engine's buffers, 1 + 4 pairs of launches each timed with
+// HIP events (on a random field, see below); the fastest by its median pair
+// replaces the models' plan if it is at least 3% faster (timings at
 // create scatter by ~2%: at 65536^2 a variant "2% faster" there ran the same in
 // steady state).  The variants are all plan kinds the parity tests pin, so this
 // changes speed only.  8-way rank launch shapes (one process, TCUPS, models' plan
@@ -1688,6 +1688,18 @@ gol_status autotune_plans(gol_engine* e)
     hipEvent_t t0 = nullptr, t1 = nullptr;
     HIP_TRY(hipEventCreate(&t0));
     HIP_TRY(hipEventCreate(&t1));
+    // (r04) Time the candidates as they run in a step: on a p = 0.5 field (a
+    // zero field draws less power and runs at a higher clock) and as pairs of
+    // back-to-back launches (each launch's tail overlaps the next one's start),
+    // the median of 4 pairs after one untimed pair.  At 16640 x 65536 single
+    // launches on the zero field kept the models' plan, 3.9% slower in steady state
+    // than its skew x 1.05 variant (profiles/r04/ab_plan_variants_forced.jsonl).
+    // The field is zeroed again afterwards: a new engine holds a dead field.
+    const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
+    HIP_TRY(gol::launch_init_random(e->buf[e->cur], (int64_t)e->stride, (int64_t)e->wq,
+                                    e->lastmask, 0, 0, (int64_t)e->buf_rows, 0x5eedull,
+                                    e->planes, e->stream));
+    constexpr int kPairs = 4;
     gol_status st = GOL_OK;
     for (size_t pi = 0; pi < e->plan_alts.size() && st == GOL_OK; ++pi) {
         auto& alts = e->plan_alts[pi];
@@ -1695,18 +1707,24 @@ gol_status autotune_plans(gol_engine* e)
         std::vector<gol_engine::Plan> cand{e->plans[pi]};
         cand.insert(cand.end(), alts.begin(), alts.end());
         alts.clear();
-        std::vector<float> best(cand.size(), 1e30f);
-        for (int rep = 0; rep < 6 && st == GOL_OK; ++rep)
+        std::vector<std::vector<float>> times(cand.size());
+        for (int rep = 0; rep <= kPairs && st == GOL_OK; ++rep)
             for (size_t c = 0; c < cand.size() && st == GOL_OK; ++c) {
                 e->plans[pi] = cand[c];
                 float ms = 0;
                 if (hipEventRecord(t0, e->stream) != hipSuccess) st = fail(GOL_EHIP, "autotune event");
-                if (st == GOL_OK) st = launch(e, (int)pi, e->K, false);
+                for (int l = 0; l < 2 && st == GOL_OK; ++l) st = launch(e, (int)pi, e->K, false);
                 if (st == GOL_OK && (hipEventRecord(t1, e->stream) != hipSuccess ||
                                      hipEventSynchronize(t1) != hipSuccess ||
                                      hipEventElapsedTime(&ms, t0, t1) != hipSuccess))
                     st = fail(GOL_EHIP, "autotune timing");
-                if (rep > 0) best[c] = std::min(best[c], ms);
+                if (rep > 0) times[c].push_back(0.5f * ms);
+            }
+        std::vector<float> best(cand.size(), 1e30f);
+        for (size_t c = 0; c < cand.size(); ++c)
+            if (!times[c].empty()) {
+                std::sort(times[c].begin(), times[c].end());
+                best[c] = 0.5f * (times[c][(times[c].size() - 1) / 2] + times[c][times[c].size() / 2]);
             }
         size_t pick = 0;
         for (size_t c = 1; c < cand.size(); ++c)
@@ -1726,6 +1744,9 @@ gol_status autotune_plans(gol_engine* e)
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
     if (st == GOL_OK) st = check_err(e);  // a hand-off wait that timed out is a failure here too
+    for (int b = 0; b < 2 && st == GOL_OK; ++b)
+        if (hipMemsetAsync(e->alloc[b], 0, words_all * sizeof(uint64_t), e->stream) != hipSuccess)
+            st = fail(GOL_EHIP, "autotune: clearing the field");
     return st;
 }
 
