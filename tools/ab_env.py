@@ -31,8 +31,11 @@ def main():
     p.add_argument("--gens", type=int, default=512)
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--rule", default="ref")
+    p.add_argument("--lib", default="", help="library build to load (GOL_LIB), dev A/B")
     p.add_argument("--handoff", type=int, default=0)
     a = p.parse_args()
+    if a.lib:
+        os.environ["GOL_LIB"] = os.path.abspath(a.lib)
     pkg = entry.load_package()
     rule = pkg.REF_RULE if a.rule == "ref" else pkg.CONWAY
     for sh in a.shapes.split(","):
@@ -65,6 +68,7 @@ def main():
             e.set_timing(0)
             cells = float(h) * w * a.gens
             print(json.dumps({
+                "lib": os.path.basename(os.environ.get("GOL_LIB", "libgol.so")),
                 "shape": f"{h}x{w}", "rule": a.rule, a.var: v,
                 "handoff": e.handoff, "tb_depth": e.tb_depth, "rows_per_wave": e.rows_per_wave,
                 "age_skew": e.age_skew, "gens": a.gens,

@@ -82,11 +82,14 @@ def main():
     p.add_argument("--handoff", type=int, default=0, help="gol_config.handoff")
     p.add_argument("--overlaps", default="0", help="gol_config.exchange_overlap values "
                    "(0 auto = blocking for rank engines, 1 blocking, 2 overlapped)")
+    p.add_argument("--lib", default="", help="library build to load (GOL_LIB), dev A/B")
     p.add_argument("--transports", default="noop", help="noop and/or rccl (self-loop)")
     p.add_argument("--halo-depths", default="0", help="gol_config.halo_depth values (0 = auto)")
     p.add_argument("--shrinks", default="0", help="GOL_DEV_RANK_SHRINK values: 0 = one region "
                    "for the full-depth launches of a round (default), 1 = shrinking regions")
     a = p.parse_args()
+    if a.lib:
+        os.environ["GOL_LIB"] = os.path.abspath(a.lib)
     pkg = entry.load_package()
     n = a.size
     tp, keep = noop_transport(pkg)  # noqa: F841 (keeps the library and callback alive)
@@ -119,7 +122,7 @@ def main():
         for sk, e, ts in engines:
             t = statistics.median(ts)
             rate = e.rows * n * a.gens / t / 1e12
-            print(json.dumps({"size": n, "nranks": N, "rank": rank, "own_rows": e.rows,
+            print(json.dumps({"lib": os.path.basename(os.environ.get("GOL_LIB", "libgol.so")), "size": n, "nranks": N, "rank": rank, "own_rows": e.rows,
                               "halo_depth": e.halo_depth, "tb_depth": e.tb_depth,
                               "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
                               "age_skew": e.age_skew, "skew_cfg": sk[0], "overlap_cfg": sk[1],
