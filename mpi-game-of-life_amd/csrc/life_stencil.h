@@ -208,11 +208,21 @@ __device__ __forceinline__ uint32_t right_of(const Pl<NP>& x, const Ends& e, int
 // directly:
 //   REF (B/S2):      next = alive && T == 3   (Parallel_Life_MPI.cpp:47-50)
 //   CONWAY (B3/S23): next = T == 3 || (alive && T == 4)
+//
+// B/S2 shares work between a stage's consecutive steps (r04, GOL_PAIR_SUM): rows
+// r-1 and r emitted at two consecutive steps both see the pair H3(r-1) + H3(r)
+// (ingest of r: emit r-1 = pair + H3(r-2); ingest of r+1: emit r = pair + H3(r+1)).
+// The pair sum P = q0 + 2 q1 + 4 q2 (0..6) is formed once, at the step whose
+// ingested row has even index (a "pair step"), and kept in (q0, q1, q2) for the
+// next one.  For a third row A = a0 + 2 a1 (0..3), T = P + A == 3 exactly when
+// q2 = 0, q1 = !a1 and q0 = !a0: three v_bitop3 per plane instead of six, and four
+// for the pair every second step -- 7 instead of 8 per plane and stage-step.
 template <int NP>
 struct StageT {
     Pl<NP> ps, pc;
     Pl<NP> cs, cc;
     Pl<NP> al;
+    Pl<NP> q0, q1, q2;  // B/S2: the pair sum between a pair step and the next step
 };
 
 template <int RULE>
@@ -256,11 +266,32 @@ __device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint3
     }
 }
 
+#ifndef GOL_PAIR_SUM
+#define GOL_PAIR_SUM 1
+#endif
+constexpr uint32_t kXor2 = 0x3C;        // a ^ b
+constexpr uint32_t kAnd2 = 0xC0;        // a & b
+constexpr uint32_t kNotAndXor = 0x06;   // ~a & (b ^ c)
+constexpr uint32_t kAndXor = 0x60;      // a & (b ^ c)
+
+// B/S2 of one plane from the pair sum (q0, q1, q2), the third row's H3 (a0, a1)
+// and the cell: alive && P + A == 3
+__device__ __forceinline__ uint32_t ref_from_pair(uint32_t q0, uint32_t q1, uint32_t q2,
+                                                  uint32_t a0, uint32_t a1, uint32_t alive)
+{
+    const uint32_t u = lop3<kNotAndXor>(q2, q1, a1);
+    const uint32_t v = lop3<kAndXor>(alive, q0, a0);
+    return lop3<kAnd2>(u, v, v);
+}
+
 // One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
+// `pair`: the step forms the B/S2 pair sum (even ingested row; a constant once the
+// caller's loops are unrolled).
 template <int RULE, int NP>
 __device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, uint32_t birth,
-                                             uint32_t survive)
+                                             uint32_t survive, bool pair)
 {
+    constexpr bool kPairSum = RULE == RULE_REF && GOL_PAIR_SUM;
     const Ends e = ends(x);
     Pl<NP> s3, c3, y;
 #pragma unroll
@@ -268,11 +299,31 @@ __device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, ui
         const uint32_t L = left_of(x, e, k), R = right_of(x, e, k);
         s3.v[k] = lop3<kXor3>(L, x.v[k], R);
         c3.v[k] = lop3<kMaj>(L, x.v[k], R);
-        y.v[k] = rule32_total<RULE>(st.ps.v[k], st.pc.v[k], st.cs.v[k], st.cc.v[k], s3.v[k],
-                                    c3.v[k], st.al.v[k], birth, survive);
+        if constexpr (kPairSum) {
+            if (pair) {
+                // P = H3(r-1) + H3(r); emit r-1 against H3(r-2)
+                const uint32_t q0 = lop3<kXor2>(st.cs.v[k], s3.v[k], s3.v[k]);
+                const uint32_t cy = lop3<kAnd2>(st.cs.v[k], s3.v[k], s3.v[k]);
+                const uint32_t q1 = lop3<kXor3>(st.cc.v[k], c3.v[k], cy);
+                const uint32_t q2 = lop3<kMaj>(st.cc.v[k], c3.v[k], cy);
+                y.v[k] = ref_from_pair(q0, q1, q2, st.ps.v[k], st.pc.v[k], st.al.v[k]);
+                st.q0.v[k] = q0;
+                st.q1.v[k] = q1;
+                st.q2.v[k] = q2;
+            } else {
+                // P = H3(r-2) + H3(r-1) from the pair step; emit r-1 against H3(r)
+                y.v[k] = ref_from_pair(st.q0.v[k], st.q1.v[k], st.q2.v[k], s3.v[k], c3.v[k],
+                                       st.al.v[k]);
+            }
+        } else {
+            y.v[k] = rule32_total<RULE>(st.ps.v[k], st.pc.v[k], st.cs.v[k], st.cc.v[k], s3.v[k],
+                                        c3.v[k], st.al.v[k], birth, survive);
+        }
     }
-    st.ps = st.cs;
-    st.pc = st.cc;
+    if (!kPairSum || !pair) {
+        st.ps = st.cs;
+        st.pc = st.cc;
+    }
     st.cs = s3;
     st.cc = c3;
     st.al = x;
@@ -345,9 +396,12 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 #endif
 
 template <int K, int RULE, int NP, bool HAND, int TOFF>
-// (the 8-step-prefetch hand-off kernels of tail offset 2 need 258 VGPRs: capped to
-// keep 2 waves per SIMD, with a few scratch spills)
-__global__ __launch_bounds__(256, (HAND && TOFF == 2 && kPfOf<NP, K>() == 8 && RULE != RULE_GENERIC) ? 2 : 1)
+// (capped at 256 registers to keep 2 waves per SIMD: the 8-step-prefetch hand-off
+// kernels of tail offset 2, which need 258 VGPRs, with a few scratch spills, and the
+// B/S2 ones with the pair sum, whose hand-off kernels would take 262)
+__global__ __launch_bounds__(256, (kPfOf<NP, K>() == 8 &&
+                                   ((RULE == RULE_REF && GOL_PAIR_SUM) ||
+                                    (HAND && TOFF == 2 && RULE != RULE_GENERIC))) ? 2 : 1)
 void life_tb_kernel(StepArgs a)
 {
     constexpr bool kBirths = RULE != RULE_REF;
@@ -543,16 +597,19 @@ void life_tb_kernel(StepArgs a)
     auto row_mask = [&](int32_t r) -> uint32_t {  // r: field row relative to glob0 + row_first
         return __builtin_amdgcn_readfirstlane((r >= f_lo) && (r < f_hi) ? ~0u : 0u);
     };
-    auto stage_rm = [&](int g, Pl<NP> x, uint32_t rm, auto masked) -> Pl<NP> {
-        x = stage_step<RULE>(st[g], x, a.birth, a.survive);
+    // (the ingested row of stage g at step t is t - g; every caller's t has the parity
+    // of its unrolled step index p: blocks start at multiples of kPrefetch, the tail
+    // at t_side = R + 2 with R even for hand-off plans)
+    auto stage_rm = [&](int g, int p, Pl<NP> x, uint32_t rm, auto masked) -> Pl<NP> {
+        x = stage_step<RULE>(st[g], x, a.birth, a.survive, ((p - g) & 1) == 0);
         if constexpr (kBirths && decltype(masked)::value) {
 #pragma unroll
             for (int k = 0; k < NP; ++k) x.v[k] = lop3<kAnd3>(x.v[k], cm.v[k], rm);
         }
         return x;
     };
-    auto stage = [&](int g, int32_t t, Pl<NP> x) -> Pl<NP> {
-        return stage_rm(g, x, kBirths ? row_mask(t - (g + 1)) : 0u, std::true_type{});
+    auto stage = [&](int g, int p, int32_t t, Pl<NP> x) -> Pl<NP> {
+        return stage_rm(g, p, x, kBirths ? row_mask(t - (g + 1)) : 0u, std::true_type{});
     };
     // Steady blocks without the births mask (r04).  The mask only changes cells the
     // unit holds outside the field: lanes outside it or bits >= w of the last
@@ -681,7 +738,7 @@ void life_tb_kernel(StepArgs a)
             for (int p = 0; p < kPrefetch; ++p) {
                 const int g = d - p;
                 if (g >= 0 && g < K && (!kGuard || t0 + p >= 2 * g)) {
-                    x[p] = stage_rm(g, x[p], kMask ? rmv[p - g - 1 + K] : 0u,
+                    x[p] = stage_rm(g, p, x[p], kMask ? rmv[p - g - 1 + K] : 0u,
                                     std::integral_constant<bool, kMask>{});
                     if constexpr (HAND && kGuard && !(GOL_EXP & 4)) {
                         if (g <= K - 2 && (t0 + p == 2 * g + 2 || t0 + p == 2 * g + 3))
@@ -782,7 +839,7 @@ void life_tb_kernel(StepArgs a)
 #pragma unroll
                     for (int p = 0; p < TOFF; ++p) {
                         const int g = d - p;
-                        if (g >= 0 && g < K) x[p] = stage(g, t0 + p, x[p]);
+                        if (g >= 0 && g < K) x[p] = stage(g, p, t0 + p, x[p]);
                     }
                 }
 #pragma unroll
@@ -806,7 +863,7 @@ void life_tb_kernel(StepArgs a)
                     for (int p = 0; p < kPrefetch; ++p) {
                         const int g = d - p, tau = tau0 + p;
                         if (tau < kSideRows && g >= tau / 2 + 1 && g < K)
-                            x[p] = stage(g, tb + tau, x[p]);
+                            x[p] = stage(g, p, tb + tau, x[p]);
                     }
                 }
 #pragma unroll

@@ -46,7 +46,10 @@ def config_of(log):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("prof_dir")
-    p.add_argument("--out", default="profiles/r03/counters.json")
+    p.add_argument("--out", default="profiles/r04/counters.json")
+    p.add_argument("--stage-rev", type=int, default=2,
+                   help="stage-logic revision of the profiled build (bench.py STAGE_REV; "
+                        "2 = B/S2 pair sum, r04)")
     a = p.parse_args()
     d = a.prof_dir
     cfg = config_of(os.path.join(d, "pmc_FETCH_SIZE.log"))
@@ -89,13 +92,15 @@ def main():
             rec["trace_kernel"] = top["Name"]
             rec["trace_avg_launch_ns"] = float(top["AverageNs"])
             rec["trace_calls"] = int(top["Calls"])
+    if cfg.get("rule") == "ref":
+        rec["stage_rev"] = a.stage_rev
     rec["source"] = os.path.basename(os.path.normpath(d))
     rec["source_round"] = os.path.basename(os.path.dirname(os.path.abspath(a.out)))
     doc = {"records": []}
     if os.path.exists(a.out):
         doc = json.load(open(a.out))
-    keys = ("size", "rule", "tb_depth", "streams", "n_gpus", "rows_per_wave", "handoff")
-    doc["records"] = [r for r in doc["records"] if not all(r.get(k) == rec[k] for k in keys)]
+    keys = ("stage_rev", "size", "rule", "tb_depth", "streams", "n_gpus", "rows_per_wave", "handoff")
+    doc["records"] = [r for r in doc["records"] if not all(r.get(k) == rec.get(k) for k in keys)]
     doc["records"].append(rec)
     doc["_doc"] = ("Per-launch counters of the stencil kernel (life_tb_kernel, or life_res_kernel "
                    "for resident fields) by configuration: rocprofv3 --pmc "
