@@ -1,0 +1,112 @@
+"""The stage logic's v_bitop3 networks, checked exhaustively on the CPU.
+
+life_stencil.h computes each generation with 3-input bitwise functions
+(v_bitop3_b32, truth table in an 8-bit immediate).  This test reads the immediates
+from the header and evaluates the networks bit-sliced over every case they can
+meet, against the rule itself (Parallel_Life_MPI.cpp:37-54, restated in
+oracle/gol_oracle.c):
+
+  * the 3-row total T = H3(r-2) + H3(r-1) + H3(r) of rule32_total (B/S2, B3/S23);
+  * the r04 pair sum of B/S2 (GOL_PAIR_SUM): P = H3(r-1) + H3(r) = q0 + 2 q1 + 4 q2
+    formed once for two rows, then alive && P + A == 3 for either third row A.
+"""
+import itertools
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "mpi-game-of-life_amd", "csrc", "life_stencil.h")
+
+
+def luts():
+    src = open(HDR).read()
+    return {m.group(1): int(m.group(2), 16)
+            for m in re.finditer(r"constexpr uint32_t (k\w+) = 0x([0-9A-Fa-f]+);", src)}
+
+
+def bitop3(lut, a, b, c):
+    """v_bitop3_b32 on 0/1 inputs: the immediate is the truth table evaluated on
+    S0 = 0xF0, S1 = 0xCC, S2 = 0xAA, i.e. bit index 4a + 2b + c."""
+    return (lut >> (4 * a + 2 * b + c)) & 1
+
+
+def h3(left, mid, right):
+    """(sum, carry) of a cell and its two horizontal neighbours, as the kernel forms them."""
+    L = luts()
+    return bitop3(L["kXor3"], left, mid, right), bitop3(L["kMaj"], left, mid, right)
+
+
+def triples():
+    return list(itertools.product((0, 1), repeat=3))
+
+
+def test_h3_is_the_horizontal_sum():
+    for t in triples():
+        s, c = h3(*t)
+        assert s + 2 * c == sum(t)
+
+
+def test_pair_sum_rule_matches_b_s2():
+    """Every (row r-2, r-1, r, r+1) horizontal triple and cell: the pair step's
+    output (row r-1 against H3(r-2)) and the next step's (row r against H3(r+1))
+    equal alive && n == 2 with n the 8-neighbour count."""
+    L = luts()
+    assert GOL_PAIR_SUM_ON()
+
+    def pair(cs, cc, s3, c3):
+        q0 = bitop3(L["kXor2"], cs, s3, s3)
+        cy = bitop3(L["kAnd2"], cs, s3, s3)
+        q1 = bitop3(L["kXor3"], cc, c3, cy)
+        q2 = bitop3(L["kMaj"], cc, c3, cy)
+        return q0, q1, q2
+
+    def test(q0, q1, q2, a0, a1, alive):
+        u = bitop3(L["kNotAndXor"], q2, q1, a1)
+        v = bitop3(L["kAndXor"], alive, q0, a0)
+        return bitop3(L["kAnd2"], u, v, v)
+
+    n = 0
+    for up, mid, low, low2 in itertools.product(triples(), repeat=4):
+        a = h3(*up)      # H3(r-2)
+        b = h3(*mid)     # H3(r-1): the row emitted at the pair step
+        e = h3(*low)     # H3(r): the row emitted at the next step
+        f = h3(*low2)    # H3(r+1)
+        q = pair(b[0], b[1], e[0], e[1])
+        assert q[0] + 2 * q[1] + 4 * q[2] == sum(mid) + sum(low)
+        # pair step: row r-1 (cell mid[1]) sees rows r-2, r-1, r
+        nb = sum(up) + sum(mid) + sum(low) - mid[1]
+        assert test(*q, a[0], a[1], mid[1]) == int(mid[1] == 1 and nb == 2)
+        # next step: row r (cell low[1]) sees rows r-1, r, r+1
+        nb = sum(mid) + sum(low) + sum(low2) - low[1]
+        assert test(*q, f[0], f[1], low[1]) == int(low[1] == 1 and nb == 2)
+        n += 1
+    assert n == 8 ** 4
+
+
+def test_three_row_rules_match():
+    """rule32_total's B/S2 and B3/S23 networks against the rule on every 3 x 3 case."""
+    L = luts()
+
+    def total(a, b, e, alive, rule):
+        s0 = bitop3(L["kXor3"], a[0], b[0], e[0])
+        k0 = bitop3(L["kMaj"], a[0], b[0], e[0])
+        p = bitop3(L["kXor3"], a[1], b[1], e[1])
+        mj = bitop3(L["kMaj"], a[1], b[1], e[1])
+        three = bitop3(L["kTwoThree"], p, k0, mj)
+        if rule == "ref":
+            return bitop3(L["kAnd3"], alive, s0, three)
+        four = bitop3(L["kFour"], p, k0, mj)
+        stay = bitop3(L["kAndNot"], alive, four, s0)
+        return bitop3(L["kOrAnd2"], s0, three, stay)
+
+    for up, mid, low in itertools.product(triples(), repeat=3):
+        alive = mid[1]
+        nb = sum(up) + sum(mid) + sum(low) - alive
+        a, b, e = h3(*up), h3(*mid), h3(*low)
+        assert total(a, b, e, alive, "ref") == int(alive == 1 and nb == 2)
+        assert total(a, b, e, alive, "conway") == int(nb == 3 or (alive == 1 and nb == 2))
+
+
+def GOL_PAIR_SUM_ON():
+    m = re.search(r"#define GOL_PAIR_SUM (\d)", open(HDR).read())
+    return m is not None and m.group(1) == "1"
