@@ -172,6 +172,20 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     uint32_t* const prog_top = reinterpret_cast<uint32_t*>(zero4 + 64);
     uint32_t* const prog_bot = prog_top + W * 64;
     if (wv == 0) zero4[lane] = uint4{0u, 0u, 0u, 0u};
+    // B/S2 (r04, GOL_PAIR_SUM): the pair sums of the two rows at each edge are formed
+    // before the edges arrive, so an edge row is 3 v_bitop3 per plane once its
+    // neighbour's H3 is in (life_stencil.h ref_from_pair), and the interior rows
+    // next to them reuse the same pairs
+    constexpr bool kPair = RULE == RULE_REF && GOL_PAIR_SUM && M >= 2;
+    PairQ pt[2], pb[2];  // rows (0, 1) and (M-2, M-1)
+    auto pair_rows = [&](int i, PairQ (&q)[2]) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) q[k] = pair_sum(s[i].v[k], c[i].v[k], s[i + 1].v[k], c[i + 1].v[k]);
+    };
+    auto pair_row = [&](int i, const PairQ (&q)[2], const Pl<2>& ts, const Pl<2>& tc) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) x[i].v[k] = ref_from_pair(q[k].q0, q[k].q1, q[k].q2, ts.v[k], tc.v[k], x[i].v[k]);
+    };
     auto rule_row = [&](int i, const Pl<2>& as, const Pl<2>& ac, const Pl<2>& es,
                         const Pl<2>& ec) {
 #pragma unroll
@@ -265,9 +279,18 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
             asm volatile("" ::: "memory");  // edge reads issue after the progress reads
             uint4 tu = *pu, td = *pd;
             // interior rows first: no LDS operand, they cover the round trip
+            if constexpr (kPair) {
+                pair_rows(0, pt);
+                if constexpr (M > 2) pair_rows(M - 2, pb);
+            }
 #pragma unroll
             for (int i = 1; i < M - 1; ++i) {
-                rule_row(i, s[i - 1], c[i - 1], s[i + 1], c[i + 1]);
+                if (kPair && i == 1)
+                    pair_row(1, pt, s[M > 2 ? 2 : 0], c[M > 2 ? 2 : 0]);
+                else if (kPair && i == M - 2)
+                    pair_row(M - 2, pb, s[M > 2 ? M - 3 : 0], c[M > 2 ? M - 3 : 0]);
+                else
+                    rule_row(i, s[i - 1], c[i - 1], s[i + 1], c[i + 1]);
                 asm volatile("" : "+v"(x[i].v[0]), "+v"(x[i].v[1]));
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -290,7 +313,7 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
                 if (__builtin_amdgcn_readfirstlane((int32_t)(wd - need)) < 0) await(wait_dn, need, pd, td);
                 Pl<2> ds, dc;
                 ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
-                rule_row(0, us, uc, ds, dc);
+                rule_row(0, us, uc, ds, dc);  // (M = 1: no pair)
                 if (publish) {
                     h3_row(x[0], s[0], c[0]);
                     put_top(q);
@@ -300,7 +323,10 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
                     set_word(my_bot, need + 1u);
                 }
             } else {
-                rule_row(0, us, uc, s[1], c[1]);
+                if constexpr (kPair)
+                    pair_row(0, pt, us, uc);
+                else
+                    rule_row(0, us, uc, s[1], c[1]);
                 // the last row's rule reads row M-2's H3 of this generation: with
                 // M = 2 that is row 0's, about to be replaced
                 const Pl<2> s_up = s[M - 2], c_up = c[M - 2];
@@ -319,7 +345,12 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
 #endif
                 Pl<2> ds, dc;
                 ds.v[0] = td.x; ds.v[1] = td.y; dc.v[0] = td.z; dc.v[1] = td.w;
-                rule_row(M - 1, s_up, c_up, ds, dc);
+                if constexpr (kPair && M > 2)
+                    pair_row(M - 1, pb, ds, dc);
+                else if constexpr (kPair)
+                    pair_row(M - 1, pt, ds, dc);
+                else
+                    rule_row(M - 1, s_up, c_up, ds, dc);
                 if (publish) {
                     h3_row(x[M - 1], s[M - 1], c[M - 1]);
                     put_bot(q);

@@ -284,6 +284,20 @@ __device__ __forceinline__ uint32_t ref_from_pair(uint32_t q0, uint32_t q1, uint
     return lop3<kAnd2>(u, v, v);
 }
 
+// The pair sum of two H3 rows (b, e), one plane: q0 + 2 q1 + 4 q2 = b + e
+struct PairQ {
+    uint32_t q0, q1, q2;
+};
+__device__ __forceinline__ PairQ pair_sum(uint32_t bs, uint32_t bc, uint32_t es, uint32_t ec)
+{
+    PairQ q;
+    q.q0 = lop3<kXor2>(bs, es, es);
+    const uint32_t cy = lop3<kAnd2>(bs, es, es);
+    q.q1 = lop3<kXor3>(bc, ec, cy);
+    q.q2 = lop3<kMaj>(bc, ec, cy);
+    return q;
+}
+
 // One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
 // `pair`: the step forms the B/S2 pair sum (even ingested row; a constant once the
 // caller's loops are unrolled).
@@ -302,14 +316,11 @@ __device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, ui
         if constexpr (kPairSum) {
             if (pair) {
                 // P = H3(r-1) + H3(r); emit r-1 against H3(r-2)
-                const uint32_t q0 = lop3<kXor2>(st.cs.v[k], s3.v[k], s3.v[k]);
-                const uint32_t cy = lop3<kAnd2>(st.cs.v[k], s3.v[k], s3.v[k]);
-                const uint32_t q1 = lop3<kXor3>(st.cc.v[k], c3.v[k], cy);
-                const uint32_t q2 = lop3<kMaj>(st.cc.v[k], c3.v[k], cy);
-                y.v[k] = ref_from_pair(q0, q1, q2, st.ps.v[k], st.pc.v[k], st.al.v[k]);
-                st.q0.v[k] = q0;
-                st.q1.v[k] = q1;
-                st.q2.v[k] = q2;
+                const PairQ q = pair_sum(st.cs.v[k], st.cc.v[k], s3.v[k], c3.v[k]);
+                y.v[k] = ref_from_pair(q.q0, q.q1, q.q2, st.ps.v[k], st.pc.v[k], st.al.v[k]);
+                st.q0.v[k] = q.q0;
+                st.q1.v[k] = q.q1;
+                st.q2.v[k] = q.q2;
             } else {
                 // P = H3(r-2) + H3(r-1) from the pair step; emit r-1 against H3(r)
                 y.v[k] = ref_from_pair(st.q0.v[k], st.q1.v[k], st.q2.v[k], s3.v[k], c3.v[k],
