@@ -133,7 +133,9 @@ constexpr bool handoff_toff_exists(int off, int pf)
 // A consumer block of R rows streams R + 2 input steps after the warm-up, i.e.
 // (R + 2 - warm) mod prefetch must be an offset with a kernel, and at least two
 // whole steady blocks must precede the tail (the flag wait sits at the end of the
-// first of them).  Returns the offset, or -1 if R does not fit.
+// first of them).  Returns the offset, or -1 if R does not fit.  Every offset with
+// a kernel, the warm-up and the prefetch are even, so R is even: the B/S2 pair sum
+// (life_stencil.h) relies on the tail starting at an even step t_side = R + 2.
 constexpr int handoff_toff(int64_t R, int K, int planes)
 {
     const int pf = prefetch_of(K, planes), warm = warm_steps_of(K, planes);
