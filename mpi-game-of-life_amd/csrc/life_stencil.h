@@ -410,7 +410,8 @@ template <int K, int RULE, int NP, bool HAND, int TOFF>
 // (capped at 256 registers to keep 2 waves per SIMD: the 8-step-prefetch hand-off
 // kernels of tail offset 2, which need 258 VGPRs, with a few scratch spills, and the
 // B/S2 ones with the pair sum, whose hand-off kernels would take 262)
-__global__ __launch_bounds__(256, (kPfOf<NP, K>() == 8 &&
+// (depths > 16, dev build only, need 1 wave per SIMD and stay uncapped)
+__global__ __launch_bounds__(256, (kPfOf<NP, K>() == 8 && K <= 16 &&
                                    ((RULE == RULE_REF && GOL_PAIR_SUM) ||
                                     (HAND && TOFF == 2 && RULE != RULE_GENERIC))) ? 2 : 1)
 void life_tb_kernel(StepArgs a)
