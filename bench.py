@@ -62,10 +62,10 @@ CELLS_PER_WAVE_INSTR = 64 * 64  # 64 lanes x one 64-column lane group (2 planes)
 # VALU issue slots per lane group and generation of the stage logic (v_bitop3 = 1,
 # DPP move and v_alignbit = 2 each): tools/valu_mix.py, profiles/r02/valu_mix.json
 STAGE_SLOTS = {"ref": 24, "conway": 28}
-# ... and the slots the kernel actually issues for them (r04: B/S2 forms the vertical
-# pair sum once per two rows, life_stencil.h GOL_PAIR_SUM: 14 v_bitop3 + 2 DPP moves
-# + 2 v_alignbit per lane group and generation on average)
-ISSUED_SLOTS = {"ref": 22, "conway": 28}
+# ... and the slots the kernel actually issues for them (r04: both rules form the
+# vertical pair sum once per two rows, life_stencil.h GOL_PAIR_SUM: B/S2 14 v_bitop3,
+# B3/S23 18, + 2 DPP moves + 2 v_alignbit per lane group and generation on average)
+ISSUED_SLOTS = {"ref": 22, "conway": 26}
 
 
 def parse():
@@ -112,9 +112,9 @@ def valu_mix_rate():
     return v * 10.0 / 8.0 if v else None
 
 
-# revision of the stage logic whose counters a record holds: 2 = B/S2 with the
+# revision of the stage logic whose counters a record holds (per rule): 2 = the
 # shared pair sum (r04); records without the field are revision 1
-STAGE_REV = {"ref": 2, "conway": 1}
+STAGE_REV = {"ref": 2, "conway": 2}
 
 
 def counters_for(cfg):

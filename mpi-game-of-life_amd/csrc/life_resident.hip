@@ -172,19 +172,24 @@ __global__ __launch_bounds__(1024) void life_res_kernel(ResArgs a)
     uint32_t* const prog_top = reinterpret_cast<uint32_t*>(zero4 + 64);
     uint32_t* const prog_bot = prog_top + W * 64;
     if (wv == 0) zero4[lane] = uint4{0u, 0u, 0u, 0u};
-    // B/S2 (r04, GOL_PAIR_SUM): the pair sums of the two rows at each edge are formed
-    // before the edges arrive, so an edge row is 3 v_bitop3 per plane once its
-    // neighbour's H3 is in (life_stencil.h ref_from_pair), and the interior rows
-    // next to them reuse the same pairs
-    constexpr bool kPair = RULE == RULE_REF && GOL_PAIR_SUM && M >= 2;
+    // B/S2 and B3/S23 (r04, GOL_PAIR_SUM): the pair sums of the two rows at each edge
+    // are formed before the edges arrive, so an edge row is 3 (B/S2) or 4 (B3/S23)
+    // v_bitop3 per plane once its neighbour's H3 is in (life_stencil.h
+    // rule_from_pair), and the interior rows next to them reuse the same pairs
+    constexpr bool kPair = pair_rule(RULE) && M >= 2;
     PairQ pt[2], pb[2];  // rows (0, 1) and (M-2, M-1)
     auto pair_rows = [&](int i, PairQ (&q)[2]) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) q[k] = pair_sum(s[i].v[k], c[i].v[k], s[i + 1].v[k], c[i + 1].v[k]);
+        for (int k = 0; k < 2; ++k)
+            q[k] = pair_sum<RULE>(s[i].v[k], c[i].v[k], s[i + 1].v[k], c[i + 1].v[k]);
     };
     auto pair_row = [&](int i, const PairQ (&q)[2], const Pl<2>& ts, const Pl<2>& tc) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) x[i].v[k] = ref_from_pair(q[k].q0, q[k].q1, q[k].q2, ts.v[k], tc.v[k], x[i].v[k]);
+        for (int k = 0; k < 2; ++k) {
+            uint32_t y = rule_from_pair<RULE>(q[k], ts.v[k], tc.v[k], x[i].v[k]);
+            if constexpr (kBirths) y = lop3<kAnd3>(y, cm.v[k], rowm[i]);
+            x[i].v[k] = y;
+        }
     };
     auto rule_row = [&](int i, const Pl<2>& as, const Pl<2>& ac, const Pl<2>& es,
                         const Pl<2>& ec) {

@@ -222,7 +222,7 @@ struct StageT {
     Pl<NP> ps, pc;
     Pl<NP> cs, cc;
     Pl<NP> al;
-    Pl<NP> q0, q1, q2;  // B/S2: the pair sum between a pair step and the next step
+    Pl<NP> q0, q1, q2;  // the pair sum between a pair step and the next step
 };
 
 template <int RULE>
@@ -284,10 +284,33 @@ __device__ __forceinline__ uint32_t ref_from_pair(uint32_t q0, uint32_t q1, uint
     return lop3<kAnd2>(u, v, v);
 }
 
+// B3/S23 of one plane from the pair sum: T = P + A == 3, or alive && T == 4, in
+// 5 v_bitop3 per row (7 instead of 8 per plane and row with the pair itself).  No
+// network of 4 gates over (q0, q1, q2, a0, a1, alive) exists (tools/rule_search_pair.c,
+// exhaustive); this one was found by tools/rule_search_pair_sls.c and is checked
+// exhaustively by tests/test_stage_logic.py.  (A 5-gate network whose first gate
+// reads the pair alone, shared by both rows, exists too, but its extra state
+// plane pushed the K = 16 kernels past 256 VGPRs into spills inside the loop.)
+constexpr uint32_t kConway1 = 0x19;
+constexpr uint32_t kConway2 = 0xA5;
+constexpr uint32_t kConway3 = 0x7A;
+constexpr uint32_t kConway4 = 0x40;
+constexpr uint32_t kConway5 = 0x09;
+__device__ __forceinline__ uint32_t conway_from_pair(uint32_t q0, uint32_t q1, uint32_t q2,
+                                                     uint32_t a0, uint32_t a1, uint32_t alive)
+{
+    const uint32_t g0 = lop3<kConway1>(alive, a0, q0);
+    const uint32_t g1 = lop3<kConway2>(a1, a0, q1);
+    const uint32_t g2 = lop3<kConway3>(g1, alive, g0);
+    const uint32_t g3 = lop3<kConway4>(alive, g1, q1);
+    return lop3<kConway5>(g2, q2, g3);
+}
+
 // The pair sum of two H3 rows (b, e), one plane: q0 + 2 q1 + 4 q2 = b + e
 struct PairQ {
     uint32_t q0, q1, q2;
 };
+template <int RULE>
 __device__ __forceinline__ PairQ pair_sum(uint32_t bs, uint32_t bc, uint32_t es, uint32_t ec)
 {
     PairQ q;
@@ -297,6 +320,15 @@ __device__ __forceinline__ PairQ pair_sum(uint32_t bs, uint32_t bc, uint32_t es,
     q.q2 = lop3<kMaj>(bc, ec, cy);
     return q;
 }
+template <int RULE>
+__device__ __forceinline__ uint32_t rule_from_pair(const PairQ& q, uint32_t a0, uint32_t a1,
+                                                   uint32_t alive)
+{
+    if constexpr (RULE == RULE_CONWAY) return conway_from_pair(q.q0, q.q1, q.q2, a0, a1, alive);
+    return ref_from_pair(q.q0, q.q1, q.q2, a0, a1, alive);
+}
+// rules with a pair form
+constexpr bool pair_rule(int RULE) { return GOL_PAIR_SUM && (RULE == RULE_REF || RULE == RULE_CONWAY); }
 
 // One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
 // `pair`: the step forms the B/S2 pair sum (even ingested row; a constant once the
@@ -305,7 +337,7 @@ template <int RULE, int NP>
 __device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, uint32_t birth,
                                              uint32_t survive, bool pair)
 {
-    constexpr bool kPairSum = RULE == RULE_REF && GOL_PAIR_SUM;
+    constexpr bool kPairSum = pair_rule(RULE);
     const Ends e = ends(x);
     Pl<NP> s3, c3, y;
 #pragma unroll
@@ -316,15 +348,15 @@ __device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, ui
         if constexpr (kPairSum) {
             if (pair) {
                 // P = H3(r-1) + H3(r); emit r-1 against H3(r-2)
-                const PairQ q = pair_sum(st.cs.v[k], st.cc.v[k], s3.v[k], c3.v[k]);
-                y.v[k] = ref_from_pair(q.q0, q.q1, q.q2, st.ps.v[k], st.pc.v[k], st.al.v[k]);
+                const PairQ q = pair_sum<RULE>(st.cs.v[k], st.cc.v[k], s3.v[k], c3.v[k]);
+                y.v[k] = rule_from_pair<RULE>(q, st.ps.v[k], st.pc.v[k], st.al.v[k]);
                 st.q0.v[k] = q.q0;
                 st.q1.v[k] = q.q1;
                 st.q2.v[k] = q.q2;
             } else {
                 // P = H3(r-2) + H3(r-1) from the pair step; emit r-1 against H3(r)
-                y.v[k] = ref_from_pair(st.q0.v[k], st.q1.v[k], st.q2.v[k], s3.v[k], c3.v[k],
-                                       st.al.v[k]);
+                const PairQ q{st.q0.v[k], st.q1.v[k], st.q2.v[k]};
+                y.v[k] = rule_from_pair<RULE>(q, s3.v[k], c3.v[k], st.al.v[k]);
             }
         } else {
             y.v[k] = rule32_total<RULE>(st.ps.v[k], st.pc.v[k], st.cs.v[k], st.cc.v[k], s3.v[k],
@@ -409,10 +441,10 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 template <int K, int RULE, int NP, bool HAND, int TOFF>
 // (capped at 256 registers to keep 2 waves per SIMD: the 8-step-prefetch hand-off
 // kernels of tail offset 2, which need 258 VGPRs, with a few scratch spills, and the
-// B/S2 ones with the pair sum, whose hand-off kernels would take 262)
+// B/S2 and B3/S23 ones with the pair sum, whose hand-off kernels would take 262)
 // (depths > 16, dev build only, need 1 wave per SIMD and stay uncapped)
 __global__ __launch_bounds__(256, (kPfOf<NP, K>() == 8 && K <= 16 &&
-                                   ((RULE == RULE_REF && GOL_PAIR_SUM) ||
+                                   (pair_rule(RULE) ||
                                     (HAND && TOFF == 2 && RULE != RULE_GENERIC))) ? 2 : 1)
 void life_tb_kernel(StepArgs a)
 {

@@ -7,8 +7,9 @@ meet, against the rule itself (Parallel_Life_MPI.cpp:37-54, restated in
 oracle/gol_oracle.c):
 
   * the 3-row total T = H3(r-2) + H3(r-1) + H3(r) of rule32_total (B/S2, B3/S23);
-  * the r04 pair sum of B/S2 (GOL_PAIR_SUM): P = H3(r-1) + H3(r) = q0 + 2 q1 + 4 q2
-    formed once for two rows, then alive && P + A == 3 for either third row A.
+  * the r04 pair sum (GOL_PAIR_SUM): P = H3(r-1) + H3(r) = q0 + 2 q1 + 4 q2 formed
+    once for two rows, then B/S2 (alive && P + A == 3) or B3/S23 for either third
+    row A.
 """
 import itertools
 import os
@@ -81,6 +82,33 @@ def test_pair_sum_rule_matches_b_s2():
         assert test(*q, f[0], f[1], low[1]) == int(low[1] == 1 and nb == 2)
         n += 1
     assert n == 8 ** 4
+
+
+def test_pair_sum_rule_matches_b3_s23():
+    """The B3/S23 network on the pair sum (conway_from_pair, r04) on every
+    (row r-2, r-1, r, r+1) case: both rows of a pair equal the rule."""
+    L = luts()
+    assert GOL_PAIR_SUM_ON()
+
+    def test(q0, q1, q2, a0, a1, alive):
+        g0 = bitop3(L["kConway1"], alive, a0, q0)
+        g1 = bitop3(L["kConway2"], a1, a0, q1)
+        g2 = bitop3(L["kConway3"], g1, alive, g0)
+        g3 = bitop3(L["kConway4"], alive, g1, q1)
+        return bitop3(L["kConway5"], g2, q2, g3)
+
+    def pair(b, e):
+        q0 = bitop3(L["kXor2"], b[0], e[0], e[0])
+        cy = bitop3(L["kAnd2"], b[0], e[0], e[0])
+        return q0, bitop3(L["kXor3"], b[1], e[1], cy), bitop3(L["kMaj"], b[1], e[1], cy)
+
+    for up, mid, low, low2 in itertools.product(triples(), repeat=4):
+        q = pair(h3(*mid), h3(*low))
+        a, f = h3(*up), h3(*low2)
+        nb = sum(up) + sum(mid) + sum(low) - mid[1]
+        assert test(*q, a[0], a[1], mid[1]) == int(nb == 3 or (mid[1] == 1 and nb == 2))
+        nb = sum(mid) + sum(low) + sum(low2) - low[1]
+        assert test(*q, f[0], f[1], low[1]) == int(nb == 3 or (low[1] == 1 and nb == 2))
 
 
 def test_three_row_rules_match():

@@ -47,9 +47,9 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("prof_dir")
     p.add_argument("--out", default="profiles/r04/counters.json")
-    p.add_argument("--stage-rev", type=int, default=2,
+    p.add_argument("--stage-rev", type=int, default=0,
                    help="stage-logic revision of the profiled build (bench.py STAGE_REV; "
-                        "2 = B/S2 pair sum, r04)")
+                        "0 = the current one of the profiled rule)")
     a = p.parse_args()
     d = a.prof_dir
     cfg = config_of(os.path.join(d, "pmc_FETCH_SIZE.log"))
@@ -92,8 +92,7 @@ def main():
             rec["trace_kernel"] = top["Name"]
             rec["trace_avg_launch_ns"] = float(top["AverageNs"])
             rec["trace_calls"] = int(top["Calls"])
-    if cfg.get("rule") == "ref":
-        rec["stage_rev"] = a.stage_rev
+    rec["stage_rev"] = a.stage_rev or {"ref": 2, "conway": 2}.get(cfg.get("rule"), 1)
     rec["source"] = os.path.basename(os.path.normpath(d))
     rec["source_round"] = os.path.basename(os.path.dirname(os.path.abspath(a.out)))
     doc = {"records": []}
