@@ -24,7 +24,7 @@ prints one JSON line.
     v_bitop3 + 2 DPP moves and 2 v_alignbit at two slots each; static count of
     the steady-state loop, profiles/r02/valu_mix.json; the unit stays the r01-r03
     stage logic's count, so frac is normalised throughput: since r04 the B/S2
-    kernel issues 22 of them, valu.frac_issued) / the mean HIP-event
+    kernel issues 21 of them, valu.frac_issued) / the mean HIP-event
     launch time x concurrent streams; peak = the spec issue rate, 1024 SIMD-32 x
     2.4 GHz / 2 cycles per wave64 instruction = 1228.8 G/s (MI355X_MICROARCH.md),
     with the best measured rate beside it (profiles/r01/valu_rate.json, 1067 G/s:
@@ -62,10 +62,10 @@ CELLS_PER_WAVE_INSTR = 64 * 64  # 64 lanes x one 64-column lane group (2 planes)
 # VALU issue slots per lane group and generation of the stage logic (v_bitop3 = 1,
 # DPP move and v_alignbit = 2 each): tools/valu_mix.py, profiles/r02/valu_mix.json
 STAGE_SLOTS = {"ref": 24, "conway": 28}
-# ... and the slots the kernel actually issues for them (r04: both rules form the
-# vertical pair sum once per two rows, life_stencil.h GOL_PAIR_SUM: B/S2 14 v_bitop3,
+# ... and the slots the kernel actually issues for them (r04: both rules reduce the
+# pair of rows two outputs share once, life_stencil.h GOL_PAIR_SUM: B/S2 13 v_bitop3,
 # B3/S23 18, + 2 DPP moves + 2 v_alignbit per lane group and generation on average)
-ISSUED_SLOTS = {"ref": 22, "conway": 26}
+ISSUED_SLOTS = {"ref": 21, "conway": 26}
 
 
 def parse():
@@ -113,8 +113,9 @@ def valu_mix_rate():
 
 
 # revision of the stage logic whose counters a record holds (per rule): 2 = the
-# shared pair sum (r04); records without the field are revision 1
-STAGE_REV = {"ref": 2, "conway": 2}
+# shared pair sum (r04), 3 = B/S2's pair features (r04); records without the field
+# are revision 1
+STAGE_REV = {"ref": 3, "conway": 2}
 
 
 def counters_for(cfg):

@@ -209,14 +209,15 @@ __device__ __forceinline__ uint32_t right_of(const Pl<NP>& x, const Ends& e, int
 //   REF (B/S2):      next = alive && T == 3   (Parallel_Life_MPI.cpp:47-50)
 //   CONWAY (B3/S23): next = T == 3 || (alive && T == 4)
 //
-// B/S2 shares work between a stage's consecutive steps (r04, GOL_PAIR_SUM): rows
-// r-1 and r emitted at two consecutive steps both see the pair H3(r-1) + H3(r)
-// (ingest of r: emit r-1 = pair + H3(r-2); ingest of r+1: emit r = pair + H3(r+1)).
-// The pair sum P = q0 + 2 q1 + 4 q2 (0..6) is formed once, at the step whose
-// ingested row has even index (a "pair step"), and kept in (q0, q1, q2) for the
-// next one.  For a third row A = a0 + 2 a1 (0..3), T = P + A == 3 exactly when
-// q2 = 0, q1 = !a1 and q0 = !a0: three v_bitop3 per plane instead of six, and four
-// for the pair every second step -- 7 instead of 8 per plane and stage-step.
+// Both fixed rules share work between a stage's consecutive steps (r04,
+// GOL_PAIR_SUM): rows r-1 and r emitted at two consecutive steps both see the pair
+// H3(r-1), H3(r) (ingest of r: emit r-1 = pair + H3(r-2); ingest of r+1: emit r =
+// pair + H3(r+1)).  The pair is reduced once, at the step whose ingested row has
+// even index (a "pair step"), to three planes kept in (q0, q1, q2) for the next
+// step, and each row tests them against its third row: B/S2 3 features + 3 gates
+// per row (ref_from_pair), B3/S23 the binary pair sum q0 + 2 q1 + 4 q2 + 5 gates
+// per row (conway_from_pair).  Per plane and stage-step 6.5 instead of 8 v_bitop3
+// (B/S2) and 9 instead of 10 (B3/S23), H3 included.
 template <int NP>
 struct StageT {
     Pl<NP> ps, pc;
@@ -271,17 +272,27 @@ __device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint3
 #endif
 constexpr uint32_t kXor2 = 0x3C;        // a ^ b
 constexpr uint32_t kAnd2 = 0xC0;        // a & b
-constexpr uint32_t kNotAndXor = 0x06;   // ~a & (b ^ c)
-constexpr uint32_t kAndXor = 0x60;      // a & (b ^ c)
 
-// B/S2 of one plane from the pair sum (q0, q1, q2), the third row's H3 (a0, a1)
-// and the cell: alive && P + A == 3
-__device__ __forceinline__ uint32_t ref_from_pair(uint32_t q0, uint32_t q1, uint32_t q2,
-                                                  uint32_t a0, uint32_t a1, uint32_t alive)
+// B/S2 of one plane from a pair (b, e) = (H3 of the upper row, H3 of the lower
+// row), the third row's H3 (a0, a1) and the cell: alive && b + e + A == 3.  The
+// pair enters as three features formed once for its two rows (kRefF*, from bs, bc,
+// es) and each row tests them, the pair's lower carry ec and its own third row in
+// 3 v_bitop3 (kRefT*): 4.5 per plane and row against 5 for the binary pair sum
+// q0 + 2 q1 + 4 q2 (4 per pair) and its 3-gate test.  Found by
+// tools/rule_search_pair_feat.c, checked exhaustively by tests/test_stage_logic.py.
+constexpr uint32_t kRefF0 = 0x7B;
+constexpr uint32_t kRefF1 = 0x95;
+constexpr uint32_t kRefF2 = 0xBC;
+constexpr uint32_t kRefT0 = 0xC7;
+constexpr uint32_t kRefT1 = 0x9E;
+constexpr uint32_t kRefT2 = 0x02;
+__device__ __forceinline__ uint32_t ref_from_pair(uint32_t f0, uint32_t f1, uint32_t f2,
+                                                  uint32_t ec, uint32_t a0, uint32_t a1,
+                                                  uint32_t alive)
 {
-    const uint32_t u = lop3<kNotAndXor>(q2, q1, a1);
-    const uint32_t v = lop3<kAndXor>(alive, q0, a0);
-    return lop3<kAnd2>(u, v, v);
+    const uint32_t u = lop3<kRefT0>(a0, f2, f0);
+    const uint32_t v = lop3<kRefT1>(f1, ec, a1);
+    return lop3<kRefT2>(u, v, alive);
 }
 
 // B3/S23 of one plane from the pair sum: T = P + A == 3, or alive && T == 4, in
@@ -306,18 +317,27 @@ __device__ __forceinline__ uint32_t conway_from_pair(uint32_t q0, uint32_t q1, u
     return lop3<kConway5>(g2, q2, g3);
 }
 
-// The pair sum of two H3 rows (b, e), one plane: q0 + 2 q1 + 4 q2 = b + e
+// A pair of H3 rows (b upper, e lower), one plane, as the rule's test reads it:
+// B3/S23 the binary sum q0 + 2 q1 + 4 q2 = b + e; B/S2 the features kRefF* in
+// (q0, q1, q2) and the lower row's carry ec
 struct PairQ {
-    uint32_t q0, q1, q2;
+    uint32_t q0, q1, q2, ec;
 };
 template <int RULE>
 __device__ __forceinline__ PairQ pair_sum(uint32_t bs, uint32_t bc, uint32_t es, uint32_t ec)
 {
     PairQ q;
-    q.q0 = lop3<kXor2>(bs, es, es);
-    const uint32_t cy = lop3<kAnd2>(bs, es, es);
-    q.q1 = lop3<kXor3>(bc, ec, cy);
-    q.q2 = lop3<kMaj>(bc, ec, cy);
+    q.ec = ec;
+    if constexpr (RULE == RULE_REF) {
+        q.q0 = lop3<kRefF0>(es, bc, bs);
+        q.q1 = lop3<kRefF1>(es, bs, bc);
+        q.q2 = lop3<kRefF2>(es, bs, q.q1);
+    } else {
+        q.q0 = lop3<kXor2>(bs, es, es);
+        const uint32_t cy = lop3<kAnd2>(bs, es, es);
+        q.q1 = lop3<kXor3>(bc, ec, cy);
+        q.q2 = lop3<kMaj>(bc, ec, cy);
+    }
     return q;
 }
 template <int RULE>
@@ -325,13 +345,13 @@ __device__ __forceinline__ uint32_t rule_from_pair(const PairQ& q, uint32_t a0, 
                                                    uint32_t alive)
 {
     if constexpr (RULE == RULE_CONWAY) return conway_from_pair(q.q0, q.q1, q.q2, a0, a1, alive);
-    return ref_from_pair(q.q0, q.q1, q.q2, a0, a1, alive);
+    return ref_from_pair(q.q0, q.q1, q.q2, q.ec, a0, a1, alive);
 }
 // rules with a pair form
 constexpr bool pair_rule(int RULE) { return GOL_PAIR_SUM && (RULE == RULE_REF || RULE == RULE_CONWAY); }
 
 // One stage step: ingest row r (x, generation g-1), emit row r-1 at generation g.
-// `pair`: the step forms the B/S2 pair sum (even ingested row; a constant once the
+// `pair`: the step reduces the pair (even ingested row; a constant once the
 // caller's loops are unrolled).
 template <int RULE, int NP>
 __device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, uint32_t birth,
@@ -355,7 +375,7 @@ __device__ __forceinline__ Pl<NP> stage_step(StageT<NP>& st, const Pl<NP>& x, ui
                 st.q2.v[k] = q.q2;
             } else {
                 // P = H3(r-2) + H3(r-1) from the pair step; emit r-1 against H3(r)
-                const PairQ q{st.q0.v[k], st.q1.v[k], st.q2.v[k]};
+                const PairQ q{st.q0.v[k], st.q1.v[k], st.q2.v[k], st.cc.v[k]};
                 y.v[k] = rule_from_pair<RULE>(q, s3.v[k], c3.v[k], st.al.v[k]);
             }
         } else {

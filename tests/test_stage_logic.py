@@ -7,9 +7,9 @@ meet, against the rule itself (Parallel_Life_MPI.cpp:37-54, restated in
 oracle/gol_oracle.c):
 
   * the 3-row total T = H3(r-2) + H3(r-1) + H3(r) of rule32_total (B/S2, B3/S23);
-  * the r04 pair sum (GOL_PAIR_SUM): P = H3(r-1) + H3(r) = q0 + 2 q1 + 4 q2 formed
-    once for two rows, then B/S2 (alive && P + A == 3) or B3/S23 for either third
-    row A.
+  * the r04 pair form (GOL_PAIR_SUM): P = H3(r-1) + H3(r) = q0 + 2 q1 + 4 q2 formed
+    once for two rows (B3/S23), or three features of it (B/S2), then the rule for
+    either third row A.
 """
 import itertools
 import os
@@ -47,24 +47,24 @@ def test_h3_is_the_horizontal_sum():
         assert s + 2 * c == sum(t)
 
 
-def test_pair_sum_rule_matches_b_s2():
+def test_pair_rule_matches_b_s2():
     """Every (row r-2, r-1, r, r+1) horizontal triple and cell: the pair step's
     output (row r-1 against H3(r-2)) and the next step's (row r against H3(r+1))
-    equal alive && n == 2 with n the 8-neighbour count."""
+    equal alive && n == 2 with n the 8-neighbour count.  The pair (H3(r-1), H3(r))
+    enters as the three features of pair_sum<RULE_REF> and the lower row's carry."""
     L = luts()
     assert GOL_PAIR_SUM_ON()
 
-    def pair(cs, cc, s3, c3):
-        q0 = bitop3(L["kXor2"], cs, s3, s3)
-        cy = bitop3(L["kAnd2"], cs, s3, s3)
-        q1 = bitop3(L["kXor3"], cc, c3, cy)
-        q2 = bitop3(L["kMaj"], cc, c3, cy)
-        return q0, q1, q2
+    def pair(b, e):
+        f0 = bitop3(L["kRefF0"], e[0], b[1], b[0])
+        f1 = bitop3(L["kRefF1"], e[0], b[0], b[1])
+        f2 = bitop3(L["kRefF2"], e[0], b[0], f1)
+        return f0, f1, f2, e[1]
 
-    def test(q0, q1, q2, a0, a1, alive):
-        u = bitop3(L["kNotAndXor"], q2, q1, a1)
-        v = bitop3(L["kAndXor"], alive, q0, a0)
-        return bitop3(L["kAnd2"], u, v, v)
+    def test(f0, f1, f2, ec, a0, a1, alive):
+        u = bitop3(L["kRefT0"], a0, f2, f0)
+        v = bitop3(L["kRefT1"], f1, ec, a1)
+        return bitop3(L["kRefT2"], u, v, alive)
 
     n = 0
     for up, mid, low, low2 in itertools.product(triples(), repeat=4):
@@ -72,8 +72,7 @@ def test_pair_sum_rule_matches_b_s2():
         b = h3(*mid)     # H3(r-1): the row emitted at the pair step
         e = h3(*low)     # H3(r): the row emitted at the next step
         f = h3(*low2)    # H3(r+1)
-        q = pair(b[0], b[1], e[0], e[1])
-        assert q[0] + 2 * q[1] + 4 * q[2] == sum(mid) + sum(low)
+        q = pair(b, e)
         # pair step: row r-1 (cell mid[1]) sees rows r-2, r-1, r
         nb = sum(up) + sum(mid) + sum(low) - mid[1]
         assert test(*q, a[0], a[1], mid[1]) == int(mid[1] == 1 and nb == 2)
