@@ -64,8 +64,8 @@ CELLS_PER_WAVE_INSTR = 64 * 64  # 64 lanes x one 64-column lane group (2 planes)
 STAGE_SLOTS = {"ref": 24, "conway": 28}
 # ... and the slots the kernel actually issues for them (r04: both rules reduce the
 # pair of rows two outputs share once, life_stencil.h GOL_PAIR_SUM: B/S2 13 v_bitop3,
-# B3/S23 18, + 2 DPP moves + 2 v_alignbit per lane group and generation on average)
-ISSUED_SLOTS = {"ref": 21, "conway": 26}
+# B3/S23 16, + 2 DPP moves + 2 v_alignbit per lane group and generation on average)
+ISSUED_SLOTS = {"ref": 21, "conway": 24}
 
 
 def parse():
@@ -113,9 +113,9 @@ def valu_mix_rate():
 
 
 # revision of the stage logic whose counters a record holds (per rule): 2 = the
-# shared pair sum (r04), 3 = B/S2's pair features (r04); records without the field
-# are revision 1
-STAGE_REV = {"ref": 3, "conway": 2}
+# binary pair sum (r04), 3 = the pair features (r04); records without the field are
+# revision 1
+STAGE_REV = {"ref": 3, "conway": 3}
 
 
 def counters_for(cfg):

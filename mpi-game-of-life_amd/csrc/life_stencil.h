@@ -215,9 +215,9 @@ __device__ __forceinline__ uint32_t right_of(const Pl<NP>& x, const Ends& e, int
 // pair + H3(r+1)).  The pair is reduced once, at the step whose ingested row has
 // even index (a "pair step"), to three planes kept in (q0, q1, q2) for the next
 // step, and each row tests them against its third row: B/S2 3 features + 3 gates
-// per row (ref_from_pair), B3/S23 the binary pair sum q0 + 2 q1 + 4 q2 + 5 gates
-// per row (conway_from_pair).  Per plane and stage-step 6.5 instead of 8 v_bitop3
-// (B/S2) and 9 instead of 10 (B3/S23), H3 included.
+// per row (ref_from_pair), B3/S23 4 features + 4 gates per row (conway_from_pair).
+// Per plane and stage-step 6.5 instead of 8 v_bitop3 (B/S2) and 8 instead of 10
+// (B3/S23), H3 included.
 template <int NP>
 struct StageT {
     Pl<NP> ps, pc;
@@ -270,8 +270,6 @@ __device__ __forceinline__ uint32_t rule32_total(uint32_t as, uint32_t ac, uint3
 #ifndef GOL_PAIR_SUM
 #define GOL_PAIR_SUM 1
 #endif
-constexpr uint32_t kXor2 = 0x3C;        // a ^ b
-constexpr uint32_t kAnd2 = 0xC0;        // a & b
 
 // B/S2 of one plane from a pair (b, e) = (H3 of the upper row, H3 of the lower
 // row), the third row's H3 (a0, a1) and the cell: alive && b + e + A == 3.  The
@@ -295,31 +293,32 @@ __device__ __forceinline__ uint32_t ref_from_pair(uint32_t f0, uint32_t f1, uint
     return lop3<kRefT2>(u, v, alive);
 }
 
-// B3/S23 of one plane from the pair sum: T = P + A == 3, or alive && T == 4, in
-// 5 v_bitop3 per row (7 instead of 8 per plane and row with the pair itself).  No
-// network of 4 gates over (q0, q1, q2, a0, a1, alive) exists (tools/rule_search_pair.c,
-// exhaustive); this one was found by tools/rule_search_pair_sls.c and is checked
-// exhaustively by tests/test_stage_logic.py.  (A 5-gate network whose first gate
-// reads the pair alone, shared by both rows, exists too, but its extra state
-// plane pushed the K = 16 kernels past 256 VGPRs into spills inside the loop.)
-constexpr uint32_t kConway1 = 0x19;
-constexpr uint32_t kConway2 = 0xA5;
-constexpr uint32_t kConway3 = 0x7A;
-constexpr uint32_t kConway4 = 0x40;
-constexpr uint32_t kConway5 = 0x09;
-__device__ __forceinline__ uint32_t conway_from_pair(uint32_t q0, uint32_t q1, uint32_t q2,
+// B3/S23 of one plane from a pair (b, e) the same way: T = b + e + A == 3, or alive
+// && T == 4.  Four features per pair (kConwayF*; the first only feeds the others)
+// and a 4-gate test per row (kConwayT*): 6 per plane and row against 8 for the
+// 3-row total.  No test of <= 4 gates on the binary pair sum exists
+// (tools/rule_search_pair.c, exhaustive); this network was found by
+// tools/rule_search_pair_feat.c and is checked exhaustively by tests/test_stage_logic.py.
+constexpr uint32_t kConwayF0 = 0x1D;
+constexpr uint32_t kConwayF1 = 0x4D;
+constexpr uint32_t kConwayF2 = 0x18;
+constexpr uint32_t kConwayF3 = 0xBC;
+constexpr uint32_t kConwayT0 = 0xBC;
+constexpr uint32_t kConwayT1 = 0xB5;
+constexpr uint32_t kConwayT2 = 0x79;
+constexpr uint32_t kConwayT3 = 0x32;
+__device__ __forceinline__ uint32_t conway_from_pair(uint32_t f1, uint32_t f2, uint32_t f3,
                                                      uint32_t a0, uint32_t a1, uint32_t alive)
 {
-    const uint32_t g0 = lop3<kConway1>(alive, a0, q0);
-    const uint32_t g1 = lop3<kConway2>(a1, a0, q1);
-    const uint32_t g2 = lop3<kConway3>(g1, alive, g0);
-    const uint32_t g3 = lop3<kConway4>(alive, g1, q1);
-    return lop3<kConway5>(g2, q2, g3);
+    const uint32_t g4 = lop3<kConwayT0>(a0, f3, alive);
+    const uint32_t g5 = lop3<kConwayT1>(f2, g4, a1);
+    const uint32_t g6 = lop3<kConwayT2>(g4, f1, g5);
+    return lop3<kConwayT3>(g4, g6, alive);
 }
 
 // A pair of H3 rows (b upper, e lower), one plane, as the rule's test reads it:
-// B3/S23 the binary sum q0 + 2 q1 + 4 q2 = b + e; B/S2 the features kRefF* in
-// (q0, q1, q2) and the lower row's carry ec
+// three features in (q0, q1, q2) (kRefF* / kConwayF*) and, for B/S2, the lower
+// row's carry ec
 struct PairQ {
     uint32_t q0, q1, q2, ec;
 };
@@ -333,10 +332,10 @@ __device__ __forceinline__ PairQ pair_sum(uint32_t bs, uint32_t bc, uint32_t es,
         q.q1 = lop3<kRefF1>(es, bs, bc);
         q.q2 = lop3<kRefF2>(es, bs, q.q1);
     } else {
-        q.q0 = lop3<kXor2>(bs, es, es);
-        const uint32_t cy = lop3<kAnd2>(bs, es, es);
-        q.q1 = lop3<kXor3>(bc, ec, cy);
-        q.q2 = lop3<kMaj>(bc, ec, cy);
+        const uint32_t f0 = lop3<kConwayF0>(bs, es, es);
+        q.q0 = lop3<kConwayF1>(bc, f0, ec);
+        q.q1 = lop3<kConwayF2>(f0, ec, bc);
+        q.q2 = lop3<kConwayF3>(es, bs, q.q1);
     }
     return q;
 }

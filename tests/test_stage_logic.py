@@ -7,9 +7,8 @@ meet, against the rule itself (Parallel_Life_MPI.cpp:37-54, restated in
 oracle/gol_oracle.c):
 
   * the 3-row total T = H3(r-2) + H3(r-1) + H3(r) of rule32_total (B/S2, B3/S23);
-  * the r04 pair form (GOL_PAIR_SUM): P = H3(r-1) + H3(r) = q0 + 2 q1 + 4 q2 formed
-    once for two rows (B3/S23), or three features of it (B/S2), then the rule for
-    either third row A.
+  * the r04 pair form (GOL_PAIR_SUM): the pair H3(r-1), H3(r) reduced once for two
+    rows to three features, then the rule for either third row A.
 """
 import itertools
 import os
@@ -83,23 +82,24 @@ def test_pair_rule_matches_b_s2():
     assert n == 8 ** 4
 
 
-def test_pair_sum_rule_matches_b3_s23():
-    """The B3/S23 network on the pair sum (conway_from_pair, r04) on every
-    (row r-2, r-1, r, r+1) case: both rows of a pair equal the rule."""
+def test_pair_rule_matches_b3_s23():
+    """The B3/S23 pair form (pair_sum<RULE_CONWAY> features, conway_from_pair) on
+    every (row r-2, r-1, r, r+1) case: both rows of a pair equal the rule."""
     L = luts()
     assert GOL_PAIR_SUM_ON()
 
-    def test(q0, q1, q2, a0, a1, alive):
-        g0 = bitop3(L["kConway1"], alive, a0, q0)
-        g1 = bitop3(L["kConway2"], a1, a0, q1)
-        g2 = bitop3(L["kConway3"], g1, alive, g0)
-        g3 = bitop3(L["kConway4"], alive, g1, q1)
-        return bitop3(L["kConway5"], g2, q2, g3)
-
     def pair(b, e):
-        q0 = bitop3(L["kXor2"], b[0], e[0], e[0])
-        cy = bitop3(L["kAnd2"], b[0], e[0], e[0])
-        return q0, bitop3(L["kXor3"], b[1], e[1], cy), bitop3(L["kMaj"], b[1], e[1], cy)
+        f0 = bitop3(L["kConwayF0"], b[0], e[0], e[0])
+        f1 = bitop3(L["kConwayF1"], b[1], f0, e[1])
+        f2 = bitop3(L["kConwayF2"], f0, e[1], b[1])
+        f3 = bitop3(L["kConwayF3"], e[0], b[0], f2)
+        return f1, f2, f3
+
+    def test(f1, f2, f3, a0, a1, alive):
+        g4 = bitop3(L["kConwayT0"], a0, f3, alive)
+        g5 = bitop3(L["kConwayT1"], f2, g4, a1)
+        g6 = bitop3(L["kConwayT2"], g4, f1, g5)
+        return bitop3(L["kConwayT3"], g4, g6, alive)
 
     for up, mid, low, low2 in itertools.product(triples(), repeat=4):
         q = pair(h3(*mid), h3(*low))

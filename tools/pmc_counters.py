@@ -92,7 +92,7 @@ def main():
             rec["trace_kernel"] = top["Name"]
             rec["trace_avg_launch_ns"] = float(top["AverageNs"])
             rec["trace_calls"] = int(top["Calls"])
-    rec["stage_rev"] = a.stage_rev or {"ref": 3, "conway": 2}.get(cfg.get("rule"), 1)
+    rec["stage_rev"] = a.stage_rev or {"ref": 3, "conway": 3}.get(cfg.get("rule"), 1)
     rec["source"] = os.path.basename(os.path.normpath(d))
     rec["source_round"] = os.path.basename(os.path.dirname(os.path.abspath(a.out)))
     doc = {"records": []}
