@@ -6,8 +6,8 @@
 //   gcc -O3 -march=native -pthread -o /tmp/rsp tools/rule_search_pair.c
 //   /tmp/rsp 1 8     (rule 1 = B3/S23, 8 threads; rule 0 = B/S2 as a check: found)
 // Result: B/S2 has 3-gate networks (the kernel's ref_from_pair); B3/S23 has none
-// with 4 gates (and none with 3).  5-gate ones exist (rule_search_pair_sls.c):
-// 5 + 2 per plane and row against the 3-row total's 8 (conway_from_pair).
+// with 4 gates (and none with 3).  5-gate ones exist (rule_search_pair_sls.c);
+// the shipped form reduces the pair to other features (rule_search_pair_feat.c).
 #include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>

@@ -5,8 +5,9 @@
 // first NQ gates to the pair alone (shared by the pair's two rows).
 //   gcc -O3 -march=native -o /tmp/sls tools/rule_search_pair_sls.c -lm
 //   /tmp/sls NG SEED ITERS [NQ]      e.g. /tmp/sls 5 11 400000
-// Found (each checked exhaustively by tests/test_stage_logic.py once used): 5-gate
-// networks with NQ = 0 (life_stencil.h conway_from_pair) and NQ = 1.
+// Found: 5-gate networks with NQ = 0 and NQ = 1 (r04's first B3/S23 pair form,
+// 5 gates per row on the binary pair sum; since superseded by the 4 features +
+// 4 gates of rule_search_pair_feat.c, life_stencil.h conway_from_pair).
 #include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
