@@ -18,17 +18,19 @@ prints one JSON line.
 `roofline` names the bound that binds.  The stencil kernel is temporally blocked
 (K = 16 generations per launch) and VALU-issue bound, not HBM bound (DESIGN.md
 §4), so:
-  * bound "valu": achieved = the stage logic's VALU issue slots per second of
-    the timed launches -- cell-generations per launch / 4096 cells per
-    wave-instruction x slots per lane group and generation (24 for B/S2: 16
-    v_bitop3 + 2 DPP moves and 2 v_alignbit at two slots each; static count of
-    the steady-state loop, profiles/r02/valu_mix.json; the unit stays the r01-r03
-    stage logic's count, so frac is normalised throughput: since r04 the B/S2
-    kernel issues 21 of them, valu.frac_issued) / the mean HIP-event
-    launch time x concurrent streams; peak = the spec issue rate, 1024 SIMD-32 x
-    2.4 GHz / 2 cycles per wave64 instruction = 1228.8 G/s (MI355X_MICROARCH.md),
-    with the best measured rate beside it (profiles/r01/valu_rate.json, 1067 G/s:
-    peak_measured, frac_vs_measured);
+  * bound "valu": achieved = the VALU issue slots the stage logic actually
+    issues per second of the timed launches -- cell-generations per launch /
+    4096 cells per wave-instruction x the slots the kernel issues per lane group
+    and generation (ISSUED_SLOTS: B/S2 21 = 13 v_bitop3 + 2 DPP moves and 2
+    v_alignbit at two slots each; B3/S23 24; the pair features of
+    life_stencil.h, static count of the steady loop, tools/valu_mix.py) / the
+    mean HIP-event launch time x concurrent streams; peak = the spec issue rate,
+    1024 SIMD-32 x 2.4 GHz / 2 cycles per wave64 instruction = 1228.8 G/s
+    (MI355X_MICROARCH.md), with the best measured rate beside it
+    (profiles/r01/valu_rate.json, 1067 G/s: peak_measured, frac_vs_measured).
+    Up to r04 `frac` was priced in the r01-r03 stage logic's slot count (24 / 28,
+    STAGE_SLOTS), i.e. normalised throughput; that number stays under
+    frac_vs_r03_slot_unit;
   * valu.issue_frac: ALL VALU instructions per launch (rocprofv3 SQ_INSTS_VALU
     of this configuration, committed in profiles/r0N/counters.json: warm-up,
     masks and halo work included) at the same peak;
@@ -306,13 +308,13 @@ def timed_steps(eng, gens, steps, warmup, world, dist, torch, timing_every=8):
 
 
 def valu_frac(tm, rule):
-    """The stage logic's VALU issue slots per second of the sampled launches over
-    the spec issue rate (module docstring), and the work ratio."""
+    """The VALU issue slots the stage logic issues per second of the sampled
+    launches over the spec issue rate (module docstring), and the work ratio."""
     launches = max(tm["launches"], 1)
     launch_s = tm["kernel_ms"] / launches / 1e3
     cg = tm["cell_gens"] / launches
     streams = max(1, tm.get("streams", 1))
-    achieved = cg / CELLS_PER_WAVE_INSTR * STAGE_SLOTS[rule] * streams / max(launch_s, 1e-12)
+    achieved = cg / CELLS_PER_WAVE_INSTR * ISSUED_SLOTS[rule] * streams / max(launch_s, 1e-12)
     return (round(achieved / (SIMDS * SPEC_SLOT_RATE), 4),
             round(tm["cell_gens_computed"] / max(tm["cell_gens"], 1), 4))
 
@@ -444,7 +446,7 @@ def main():
     launch_s = avg_launch_ms / 1e3
     peak_slot_rate = SIMDS * SPEC_SLOT_RATE  # wave-instruction slots / s (spec)
     meas_slot_rate = SIMDS * valu_peak_rate()  # best measured issue rate
-    slots_per_launch = cg_per_launch / CELLS_PER_WAVE_INSTR * STAGE_SLOTS[a.rule]
+    slots_per_launch = cg_per_launch / CELLS_PER_WAVE_INSTR * ISSUED_SLOTS[a.rule]
     valu_achieved = slots_per_launch * streams / launch_s
     cfg_key = {"size": n, "rule": a.rule, "tb_depth": eng.tb_depth, "streams": streams,
                "n_gpus": world, "rows_per_wave": eng.rows_per_wave, "handoff": eng.handoff}
@@ -504,9 +506,13 @@ def main():
                 "bound": "valu",
                 "achieved": round(valu_achieved / 1e9, 1),
                 "peak": round(peak_slot_rate / 1e9, 1),
-                "unit": "G VALU issue slots/s (stage logic: v_bitop3 1 slot, DPP move and "
-                        "v_alignbit 2 slots)",
+                "unit": "G VALU issue slots/s (the slots the stage logic issues: v_bitop3 "
+                        "1 slot, DPP move and v_alignbit 2 slots)",
                 "frac": round(valu_achieved / peak_slot_rate, 4),
+                # the same rate in the r01-r03 slot unit (24 / 28 per lane group and
+                # generation): normalised throughput, the r04 headline `frac`
+                "frac_vs_r03_slot_unit": round(valu_achieved / peak_slot_rate * STAGE_SLOTS[a.rule]
+                                               / ISSUED_SLOTS[a.rule], 4),
                 "peak_from": "MI355X_MICROARCH.md: 1024 SIMD-32 x 2.4 GHz / 2 cycles per wave64 "
                              "VALU instruction",
                 "peak_measured": round(meas_slot_rate / 1e9, 1),
@@ -526,10 +532,8 @@ def main():
                 "cell_gens_per_launch": cg_per_launch,
                 "work_ratio": round(tm["cell_gens_computed"] / max(tm["cell_gens"], 1), 4),
                 "valu": {
-                    "slots_per_word_gen": STAGE_SLOTS[a.rule],
-                    "issued_slots_per_word_gen": ISSUED_SLOTS[a.rule],
-                    "frac_issued": round(valu_achieved / peak_slot_rate * ISSUED_SLOTS[a.rule]
-                                         / STAGE_SLOTS[a.rule], 4),
+                    "slots_per_word_gen": ISSUED_SLOTS[a.rule],
+                    "r03_unit_slots_per_word_gen": STAGE_SLOTS[a.rule],
                     "insts_per_launch": insts,
                     "issue_frac": (round(insts * streams / launch_s / peak_slot_rate, 4)
                                    if insts else None),

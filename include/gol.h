@@ -273,7 +273,14 @@ gol_status gol_create_rank_transport(uint64_t h, uint64_t w, const gol_config* c
  * gol_step(generations) call -- host-only, no GPU needed; gol_step executes
  * exactly this list.  halo_fresh: the previous call ended with an overlapped
  * exchange still to be waited for (0 after create/load).  Launch ops name the
- * local buffer rows they write (local row i = field row row0 - Hx + i). */
+ * local buffer rows they write (local row i = field row row0 - Hx + i).
+ * Computed is not valid: since r04 every full-depth launch of a round writes
+ * the first launch's region, so after a launch only the rows inside
+ * [shrink, buf_rows - shrink) (buf_rows = own rows + 2 Hx, shrink = this op's
+ * field) hold that generation; rows of [out_lo, out_hi) outside that range were
+ * computed from rows that were no longer valid and must not be read (an external
+ * transport moves only [Hx, 2 Hx) and [R, R + Hx) after a round's last launch,
+ * which are always valid). */
 typedef enum gol_sched_kind {
     GOL_OP_EXCHANGE = 0,       /* blocking halo exchange on the compute stream */
     GOL_OP_WAIT_EXCHANGE = 1,  /* compute waits for the overlapped exchange */
@@ -286,7 +293,8 @@ typedef struct gol_sched_op {
     uint32_t kind;      /* gol_sched_kind */
     uint32_t depth;     /* fused generations of a launch (0 otherwise) */
     uint32_t shrink;    /* halo rows consumed per side once this launch is done */
-    uint32_t nseg;      /* output row ranges of a launch: [out_lo[i], out_hi[i]) */
+    uint32_t nseg;      /* row ranges a launch writes: [out_lo[i], out_hi[i]); valid
+                           only inside [shrink, buf_rows - shrink), see above */
     int64_t out_lo[2];
     int64_t out_hi[2];
 } gol_sched_op;

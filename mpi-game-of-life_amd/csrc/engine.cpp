@@ -1616,6 +1616,11 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         a.err = e->d_err;
         a.side_slot = (int64_t)2 * (depth - 1) * 64 * (e->planes / 2);
         a.tail_off = gol::handoff_toff(p.rpw, (int)depth, e->planes);
+        // The pair forms (life_stencil.h stage_rm) take a step's pair parity from
+        // its unrolled index, which holds only while a consumer's tail starts at an
+        // even step t_side = R + 2: every hand-off block length must be even.
+        if ((p.rpw & 1) || (p.rows_old && ((p.rows_old | p.rows_young) & 1)))
+            return fail(GOL_ESTATE, "hand-off plan with an odd block length");
     }
     if (p.rows_old) {
         a.rows_per_wave = p.rows_young;

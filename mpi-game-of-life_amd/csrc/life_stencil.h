@@ -475,6 +475,11 @@ void life_tb_kernel(StepArgs a)
     static_assert(K + 2 * kPrefetch <= kGuardRows, "streaming loads must stay in the guard rows");
     static_assert(!HAND || K >= kHandoffMinDepth, "hand-off kernels start at kHandoffMinDepth");
     static_assert(TOFF >= 0 && TOFF < kPrefetch && (HAND || TOFF == 0), "tail offset");
+    // stage_rm takes a step's pair parity from its index within the unrolled block:
+    // every block start (warm-up, steady, tail offset, tail at t_side = R + 2 with R
+    // even, checked on the host in engine.cpp launch) must be an even step
+    static_assert(kPrefetch % 2 == 0 && kWarmSteps % 2 == 0 && TOFF % 2 == 0,
+                  "pair steps need even block starts");
     const int lane = threadIdx.x & 63;
     const int64_t unit =
         (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

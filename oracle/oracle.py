@@ -11,7 +11,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "liboracle.so")
+# GOL_ORACLE_LIB: another build of gol_oracle.c (tools/asan_cpu_suite.sh: the sanitizer build)
+_LIB = os.environ.get("GOL_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 
 # Rule masks: bit n set <=> a cell with n live neighbours is born / survives.
 REF_RULE = (0, 1 << 2)  # the reference's effective rule "B/S2" (Parallel_Life_MPI.cpp:44-50)

@@ -81,8 +81,12 @@ def test_c_abi_from_c(pkg, tmp_path):
         "return 0;}\n")
     exe = tmp_path / "t"
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{ROOT}/include", str(src),
-                    "-o", str(exe), f"-L{os.path.dirname(pkg.LIB_PATH)}", "-lgol",
-                    f"-Wl,-rpath,{os.path.dirname(pkg.LIB_PATH)}"], check=True)
+                    "-o", str(exe), f"-L{os.path.dirname(pkg.LIB_PATH)}",
+                    f"-l:{os.path.basename(pkg.LIB_PATH)}",  # libgol.so, or a GOL_LIB build
+                    f"-Wl,-rpath,{os.path.dirname(pkg.LIB_PATH)}"]
+                   # the sanitizer build's runtime is preloaded (tools/asan_cpu_suite.sh)
+                   + (["-Wl,--allow-shlib-undefined"] if os.environ.get("GOL_ASAN_SUITE") else []),
+                   check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
     assert out.split() == ["34", "33", "4"]
 
