@@ -127,7 +127,7 @@ def counters_for(cfg):
     skew variants move it by ~3%; at the same work ratio the counters move by well
     under 1%)."""
     recs = []
-    for rnd in ("r04", "r03", "r02"):  # newest first
+    for rnd in ("r05", "r04", "r03", "r02"):  # newest first
         recs += (load_json(f"profiles/{rnd}/counters.json") or {}).get("records", [])
     keys = ("size", "rule", "tb_depth", "streams", "n_gpus", "handoff")
     best = None
@@ -307,6 +307,36 @@ def timed_steps(eng, gens, steps, warmup, world, dist, torch, timing_every=8):
     return dt, eng.timing()
 
 
+def rank_breakdown(eng, tm, dt, steps, rank):
+    """(r05) Where one rank's step time goes, from its own timing (N > 1): the
+    stencil launches (mean HIP-event duration of the sampled launches x every
+    launch issued), the halo exchanges (HIP events around each one on its stream;
+    RCCL's stream time includes waiting for the peers), and the rest (launch gaps,
+    host work, the max-over-ranks barrier is not in it).  Rounds per step = the
+    exchanges; rows per launch = the buffer rows a full-depth launch computes
+    (own rows + 2 Hx - 2 K with the shared region, engine.cpp rank_geometry)."""
+    launches = max(tm["launches"], 1)
+    avg = tm["kernel_ms"] / launches
+    kern = avg * tm["launches_issued"] / steps
+    xch = tm["exchange_ms"] / steps
+    ms = dt / steps * 1e3
+    return {
+        "rank": rank, "own_rows": eng.rows, "row0": eng.row0, "halo_depth": eng.halo_depth,
+        "tb_depth": eng.tb_depth, "rows_per_wave": eng.rows_per_wave, "handoff": eng.handoff,
+        "age_skew": eng.age_skew, "autotune": list(eng.tuning),
+        "ms_per_step": round(ms, 3),
+        "launches_per_step": round(tm["launches_issued"] / steps, 2),
+        "rows_per_launch": round(tm["launch_rows"] / launches, 1),
+        "avg_launch_ms": round(avg, 4),
+        "own_tcups_per_launch": round(eng.rows * eng.w * eng.tb_depth / (avg * 1e-3) / 1e12, 2)
+        if avg > 0 else None,
+        "kernel_ms_per_step": round(kern, 3),
+        "exchanges_per_step": round(tm["exchanges"] / steps, 2),
+        "exchange_ms_per_step": round(xch, 3),
+        "other_ms_per_step": round(ms - kern - xch, 3),
+    }
+
+
 def valu_frac(tm, rule):
     """The VALU issue slots the stage logic issues per second of the sampled
     launches over the spec issue rate (module docstring), and the work ratio."""
@@ -399,12 +429,14 @@ def main():
         # blocking one: the same K steps, reported beside `value`
         eng = rank_engine(2)
         eng.init_random(a.seed)
-        ov_dt, _ = timed_steps(eng, a.gens, a.steps, a.warmup, world, dist, torch, 0)
+        ov_dt, ov_tm = timed_steps(eng, a.gens, a.steps, a.warmup, world, dist, torch, 8)
+        ov_per = [None] * world
+        dist.all_gather_object(ov_per, rank_breakdown(eng, ov_tm, ov_dt, a.steps, rank))
         ov_dt = max_over_ranks(ov_dt)
         eng.close()
         modes = {"overlapped": {"value": round(float(n) * n * a.gens * a.steps / ov_dt / 1e9, 2),
                                 "ms_per_step": round(ov_dt / a.steps * 1e3, 3),
-                                "halo_depth": None}}
+                                "halo_depth": None, "per_rank": ov_per}}
         eng = rank_engine(0)
     else:
         eng = pkg.Engine(n, n, streams=a.streams, **kw)
@@ -417,6 +449,10 @@ def main():
     # The events above keep a single-stream engine off its hipGraph replay (the
     # default path without timing): one more step on that path, not part of
     # `value`, shows the two agree
+    per_rank = None
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, rank_breakdown(eng, tm, dt, a.steps, rank))
     eng.set_timing(0)
     barrier()
     dt_graph = 1e30
@@ -435,7 +471,8 @@ def main():
     gcups = cell_gens / dt / 1e9
     if modes is not None:
         modes["blocking"] = {"value": round(gcups, 2), "ms_per_step": round(dt / a.steps * 1e3, 3),
-                             "halo_depth": eng.halo_depth, "default": True}
+                             "halo_depth": eng.halo_depth, "default": True,
+                             "per_rank": per_rank}
         modes["overlapped"]["halo_depth"] = eng.halo_depth
     ok = selfcheck is None or selfcheck.get("ok", True)
     # dominant kernel: the fused stencil (HIP events on each stripe's stream)

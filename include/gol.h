@@ -123,6 +123,15 @@ typedef struct gol_timing {
                                   strips' halo lanes */
     uint32_t streams;      /* stripe streams whose launches run concurrently */
     uint32_t reserved;
+    /* (r05) while timing is on: every stencil launch issued (sampled or not) and
+     * the buffer rows the sampled launches computed; rank engines also time
+     * every halo exchange with HIP events on its stream (RCCL: the stream time
+     * of ncclGroupStart..End, which includes waiting for the peers; host
+     * transport: staging + callback) */
+    uint64_t launches_issued;
+    double launch_rows;
+    uint64_t exchanges;
+    double exchange_ms;
 } gol_timing;
 
 /* Defaults: reference-effective rule, GLOBAL semantics, auto tuning. */
@@ -302,6 +311,31 @@ gol_status gol_round_schedule(uint64_t h, uint64_t w, const gol_config* cfg, int
                               int nranks, uint64_t generations, int halo_fresh,
                               gol_sched_op* ops, uint64_t cap, uint64_t* nops,
                               uint32_t* tb_depth, uint32_t* halo_depth);
+
+/* Host-only planning model (no GPU needed): the launch plans gol_create
+ * (nranks = 1: a single-stream engine) or gol_create_rank (rank of nranks)
+ * would build on a device of `cus` compute units whose stencil kernels fit
+ * occ_classic (classic blocks) / occ_hand (hand-off blocks) 256-thread
+ * workgroups per CU, as the occupancy query reports them, before the autotuner
+ * times its candidates.  Summarises the first full-depth launch plan: what the
+ * planner's tests check (tests/test_planner.py, also run under the host
+ * sanitizers) and what tools print. */
+typedef struct gol_plan_summary {
+    uint32_t tb_depth, halo_depth;
+    uint32_t plans, distinct_plans; /* launch plans built; aliases share one */
+    int64_t rows_lo, rows_hi;       /* buffer rows the plan computes */
+    int64_t rows_per_wave;          /* the block length (the young one when skewed) */
+    int32_t rows_old, units_old;    /* age-skewed blocks: old length and units (0: none) */
+    int32_t strips, lane_shift;     /* strips per row block, strip width 64 >> lane_shift */
+    int64_t total_units;            /* wavefronts of the launch */
+    int64_t half_units;             /* of which run the packed half strip */
+    int64_t blocks;                 /* row blocks per strip (summed over segments) */
+    int32_t handoff, tail_off;      /* hand-off blocks, their kernel's tail offset (-1) */
+    uint32_t candidates;            /* autotuner variants built for this plan */
+    uint32_t reserved;
+} gol_plan_summary;
+gol_status gol_plan_model(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
+                          int cus, int occ_classic, int occ_hand, gol_plan_summary* out);
 
 /* ---- Multi-GPU (or multi-stripe) inside ONE process, no RCCL ----
  * `nranks` stripe engines of one GLOBAL field (the same partition and halo

@@ -35,7 +35,7 @@ EXPORTS = [
     "gol_create_rank", "gol_create_group", "gol_group_step", "gol_plan_info",
     "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
     "gol_plan_resident", "gol_plan_skew", "gol_plan_columns", "gol_plan_tuning",
-    "gol_digest_rows", "gol_comm_info",
+    "gol_digest_rows", "gol_comm_info", "gol_plan_model",
 ]
 
 # gol_plan_tuning's variants (engine.cpp kTuneVariantNames): 0 = the models' plan
@@ -75,6 +75,25 @@ class Timing(ctypes.Structure):
         ("cell_gens_computed", ctypes.c_double),
         ("streams", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
+        ("launches_issued", ctypes.c_uint64),
+        ("launch_rows", ctypes.c_double),
+        ("exchanges", ctypes.c_uint64),
+        ("exchange_ms", ctypes.c_double),
+    ]
+
+
+class PlanSummary(ctypes.Structure):
+    _fields_ = [
+        ("tb_depth", ctypes.c_uint32), ("halo_depth", ctypes.c_uint32),
+        ("plans", ctypes.c_uint32), ("distinct_plans", ctypes.c_uint32),
+        ("rows_lo", ctypes.c_int64), ("rows_hi", ctypes.c_int64),
+        ("rows_per_wave", ctypes.c_int64),
+        ("rows_old", ctypes.c_int32), ("units_old", ctypes.c_int32),
+        ("strips", ctypes.c_int32), ("lane_shift", ctypes.c_int32),
+        ("total_units", ctypes.c_int64), ("half_units", ctypes.c_int64),
+        ("blocks", ctypes.c_int64),
+        ("handoff", ctypes.c_int32), ("tail_off", ctypes.c_int32),
+        ("candidates", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -166,6 +185,8 @@ def lib():
     L.gol_round_schedule.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32, u64, i32,
                                      ctypes.POINTER(SchedOp), u64, pu64, ctypes.POINTER(u32),
                                      ctypes.POINTER(u32)]
+    L.gol_plan_model.argtypes = [u64, u64, ctypes.POINTER(Config), i32, i32, i32, i32, i32,
+                                 ctypes.POINTER(PlanSummary)]
     for name in ["gol_create", "gol_create_rank", "gol_load_ascii", "gol_store_ascii",
                  "gol_load_packed", "gol_store_packed", "gol_init_random", "gol_step",
                  "gol_sync", "gol_digest", "gol_set_timing", "gol_get_timing",
@@ -173,7 +194,7 @@ def lib():
                  "gol_create_group", "gol_group_step", "gol_plan_info", "gol_plan_handoff",
                  "gol_plan_resident", "gol_plan_skew", "gol_plan_columns",
                  "gol_create_rank_transport", "gol_round_schedule", "gol_plan_tuning",
-                 "gol_digest_rows", "gol_comm_info"]:
+                 "gol_digest_rows", "gol_comm_info", "gol_plan_model"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -228,6 +249,17 @@ def round_schedule(h, w, rank, nranks, gens, halo_fresh=False, **cfg_kw):
             "segs": [(o.out_lo[i], o.out_hi[i]) for i in range(o.nseg)]}
            for o in arr[:n.value]]
     return ops, K.value, Hx.value
+
+
+def plan_model(h, w, rank=0, nranks=1, cus=256, occ_classic=2, occ_hand=2, **cfg_kw):
+    """gol_plan_model (host only, no GPU): the first full-depth launch plan the
+    engine would build on a device of `cus` CUs with those occupancies (256-thread
+    workgroups per CU), before the autotuner.  Returns a dict of PlanSummary."""
+    cfg = make_config(**cfg_kw)
+    out = PlanSummary()
+    _check(lib().gol_plan_model(h, w, ctypes.byref(cfg), rank, nranks, cus, occ_classic,
+                                occ_hand, ctypes.byref(out)))
+    return {k: getattr(out, k) for k, _ in PlanSummary._fields_ if k != "reserved"}
 
 
 def unique_id() -> bytes:
@@ -377,7 +409,9 @@ class Engine:
         t = Timing()
         _check(lib().gol_get_timing(self._h, ctypes.byref(t)))
         return {"launches": t.launches, "kernel_ms": t.kernel_ms, "cell_gens": t.cell_gens,
-                "cell_gens_computed": t.cell_gens_computed, "streams": t.streams}
+                "cell_gens_computed": t.cell_gens_computed, "streams": t.streams,
+                "launches_issued": t.launches_issued, "launch_rows": t.launch_rows,
+                "exchanges": t.exchanges, "exchange_ms": t.exchange_ms}
 
 
 def _make_transport(fn):

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -260,6 +261,12 @@ struct gol_engine {
     std::vector<Plan> plans;  // GLOBAL/REF: plans[0]; rank: see RankGeom
     std::vector<int> plan_alias;  // plans[i] copies plans[plan_alias[i]] (-1: own plan)
     std::vector<std::vector<Plan>> plan_alts;  // autotuner candidates per plan (build_plans)
+    // host-only planning (gol_plan_model): build_plans takes the device's CU count
+    // and occupancies from here and makes no device call or allocation
+    struct DevModel {
+        bool on = false;
+        int cus = 0, occ_c = 0, occ_h = 0;
+    } model;
 
     // row-block hand-off buffers (life_stencil.h): region 0 serves launches on
     // `stream`, region 1 those on `band_stream` (the two may run concurrently)
@@ -305,7 +312,8 @@ struct gol_engine {
     uint64_t launch_count = 0;
     std::vector<hipEvent_t> ev_free;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
-    std::vector<double> pending_cells, pending_cells_comp;
+    std::vector<double> pending_cells, pending_cells_comp, pending_rows;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_xpending;  // exchanges
     gol_timing tm{};
 };
 
@@ -685,12 +693,18 @@ void free_plan(gol_engine::Plan& q)
 
 gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& raw)
 {
-    int cus = 0;
-    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-    const int occ_c = gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, false);
-    const int occ_h = e->K >= (uint32_t)gol::kHandoffMinDepth
-                          ? gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, true)
-                          : 0;
+    int cus = 0, occ_c = 0, occ_h = 0;
+    if (e->model.on) {
+        cus = e->model.cus;
+        occ_c = e->model.occ_c;
+        occ_h = e->K >= (uint32_t)gol::kHandoffMinDepth ? e->model.occ_h : 0;
+    } else {
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
+        occ_c = gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, false);
+        occ_h = e->K >= (uint32_t)gol::kHandoffMinDepth
+                    ? gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, true)
+                    : 0;
+    }
     int64_t max_units = 0;
     bool any_hand = false;
     // the packed half strip of one-segment plans (col_layout; GOL_DEV_PAIRS=0 turns
@@ -859,9 +873,11 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                 p.pair_units = half_units(p.segs[0], p.half_rows, (int)e->K, e->planes, hs_v,
                                           &p.pairs);
                 p.total_units += p.pair_units;
-                HIP_TRY(hipMalloc(&p.dpairs, sizeof(int64_t) * p.pairs.size()));
-                HIP_TRY(hipMemcpy(p.dpairs, p.pairs.data(), sizeof(int64_t) * p.pairs.size(),
-                                  hipMemcpyHostToDevice));
+                if (!e->model.on) {
+                    HIP_TRY(hipMalloc(&p.dpairs, sizeof(int64_t) * p.pairs.size()));
+                    HIP_TRY(hipMemcpy(p.dpairs, p.pairs.data(), sizeof(int64_t) * p.pairs.size(),
+                                      hipMemcpyHostToDevice));
+                }
             }
         }
         for (const auto& sg : p.segs) {
@@ -898,6 +914,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
             hs_seg.unit0 = p.total_units - p.pair_units;
             dsegs.push_back(hs_seg);
         }
+        if (e->model.on) return GOL_OK;
         HIP_TRY(hipMalloc(&p.dev, sizeof(SegDesc) * dsegs.size()));
         HIP_TRY(hipMemcpy(p.dev, dsegs.data(), sizeof(SegDesc) * dsegs.size(),
                           hipMemcpyHostToDevice));
@@ -984,6 +1001,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
             e->plan_alts[pi].push_back(q);
         }
     }
+    if (e->model.on) return GOL_OK;
     HIP_TRY(hipMalloc(&e->d_err, sizeof(int)));
 #if GOL_EXP
     if (!g_dev_prog) {
@@ -1246,9 +1264,10 @@ void wait_release(gol_engine* e)
     e->reg_hand = e->reg_res = false;
 }
 
-// Common construction; geometry (row0, R, Hx, rank) already set.
-gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* cfg,
-                       const RankGeom* geom)
+// Host-side layout of an engine (no GPU): rule kind, depth and lane-group
+// layout, row stride and the last group's mask.  Geometry (row0, R, Hx, rank)
+// already set.
+gol_status host_layout(gol_engine* e, uint64_t h, uint64_t w, const gol_config* cfg)
 {
     e->H = h;
     e->W = w;
@@ -1283,20 +1302,15 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         gol_split_group(c, e->lastmask_split, e->planes);
     }
     e->sem = cfg->semantics;
+    return GOL_OK;
+}
 
-    if (cfg->device >= 0) HIP_TRY(hipSetDevice(cfg->device));
-    HIP_TRY(hipGetDevice(&e->device));
-    HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    if (e->nranks > 1) {
-        HIP_TRY(hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&e->band_stream, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_band, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_xdone, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
-    }
-
-    std::vector<std::vector<SegDesc>> raw;
+// The raw launch regions of an engine (host only): rank engines the round's
+// regions (rank_geometry), REF_STRIPES the P independent stripes, GLOBAL the
+// field; with the load/store row mappings.
+gol_status raw_regions(gol_engine* e, uint64_t h, const gol_config* cfg, const RankGeom* geom,
+                       std::vector<std::vector<SegDesc>>& raw)
+{
     if (e->nranks > 1) {
         e->buf_rows = geom->buf_rows;
         e->overlap = geom->overlap;
@@ -1341,6 +1355,28 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
         e->user_regions.push_back({0, 0, 0, h});
         e->load_regions = e->user_regions;
     }
+    return GOL_OK;
+}
+
+// Common construction; geometry (row0, R, Hx, rank) already set.
+gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* cfg,
+                       const RankGeom* geom)
+{
+    GOL_TRY(host_layout(e, h, w, cfg));
+    if (cfg->device >= 0) HIP_TRY(hipSetDevice(cfg->device));
+    HIP_TRY(hipGetDevice(&e->device));
+    HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    if (e->nranks > 1) {
+        HIP_TRY(hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&e->band_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_band, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_xdone, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+    }
+
+    std::vector<std::vector<SegDesc>> raw;
+    GOL_TRY(raw_regions(e, h, cfg, geom, raw));
 
     const size_t words = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
     for (int b = 0; b < 2; ++b) {
@@ -1409,12 +1445,24 @@ gol_status flush_timing(gol_engine* e)
         e->tm.kernel_ms += ms;
         e->tm.cell_gens += e->pending_cells[i];
         e->tm.cell_gens_computed += e->pending_cells_comp[i];
+        e->tm.launch_rows += e->pending_rows[i];
+        e->ev_free.push_back(p.first);
+        e->ev_free.push_back(p.second);
+    }
+    for (auto& p : e->ev_xpending) {
+        HIP_TRY(hipEventSynchronize(p.second));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.first, p.second));
+        e->tm.exchanges += 1;
+        e->tm.exchange_ms += ms;
         e->ev_free.push_back(p.first);
         e->ev_free.push_back(p.second);
     }
     e->ev_pending.clear();
+    e->ev_xpending.clear();
     e->pending_cells.clear();
     e->pending_cells_comp.clear();
+    e->pending_rows.clear();
     return GOL_OK;
 }
 
@@ -1433,6 +1481,7 @@ gol_status get_event(gol_engine* e, hipEvent_t* ev)
 gol_status timing_begin(gol_engine* e, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1)
 {
     *e0 = *e1 = nullptr;
+    if (e->timing_every) e->tm.launches_issued += 1;
     if (!e->timing_every || (e->launch_count++ % e->timing_every) != 0) return GOL_OK;
     GOL_TRY(get_event(e, e0));
     GOL_TRY(get_event(e, e1));
@@ -1441,13 +1490,14 @@ gol_status timing_begin(gol_engine* e, hipStream_t s, hipEvent_t* e0, hipEvent_t
 }
 
 gol_status timing_end(gol_engine* e, hipStream_t s, hipEvent_t e0, hipEvent_t e1, double own,
-                      double computed)
+                      double computed, double rows = 0)
 {
     if (!e0) return GOL_OK;
     HIP_TRY(hipEventRecord(e1, s));
     e->ev_pending.push_back({e0, e1});
     e->pending_cells.push_back(own);
     e->pending_cells_comp.push_back(computed);
+    e->pending_rows.push_back(rows);
     return GOL_OK;
 }
 
@@ -1657,8 +1707,10 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         for (size_t i = 0; i + 2 < p.pairs.size(); i += 3)
             comp_half += depth * (double)p.pairs[i + 2] + depth * (depth - 1.0);
         const double cols = 64.0 * 32.0 * e->planes;  // per strip or unit
+        double rows = 0;
+        for (const auto& sg : p.segs) rows += (double)std::max<int64_t>(0, sg.out_hi - sg.out_lo);
         GOL_TRY(timing_end(e, s, e0, e1, p.own_rows * (double)e->W * depth,
-                           (comp * p.groups + comp_half) * cols));
+                           (comp * p.groups + comp_half) * cols, rows));
     }
     if (swap) e->cur ^= 1;
     return GOL_OK;
@@ -1820,7 +1872,24 @@ gol_status check_err(gol_engine* e)
 // Halo exchange (replaces exchangeGridData, Parallel_Life_MPI.cpp:104-145, whose
 // receives land in copies): Hx rows each way with the up/down neighbour, over
 // RCCL or through the caller's host transport.
+gol_status exchange_body(gol_engine* e, hipStream_t st);
+
+// An exchange, timed with HIP events on its stream while timing is on (every
+// exchange: a few per 1000 generations).
 gol_status exchange(gol_engine* e, hipStream_t st)
+{
+    if (!e->timing_every) return exchange_body(e, st);
+    hipEvent_t e0, e1;
+    GOL_TRY(get_event(e, &e0));
+    GOL_TRY(get_event(e, &e1));
+    HIP_TRY(hipEventRecord(e0, st));
+    GOL_TRY(exchange_body(e, st));
+    HIP_TRY(hipEventRecord(e1, st));
+    e->ev_xpending.push_back({e0, e1});
+    return GOL_OK;
+}
+
+gol_status exchange_body(gol_engine* e, hipStream_t st)
 {
     uint64_t* b = e->buf[e->cur];
     const size_t n = (size_t)e->Hx * e->stride;
@@ -2016,6 +2085,71 @@ gol_status gol_round_schedule(uint64_t h, uint64_t w, const gol_config* cfg, int
             ops[i] = o;
         }
     }
+    return GOL_OK;
+}
+
+gol_status gol_plan_model(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
+                          int cus, int occ_classic, int occ_hand, gol_plan_summary* out)
+{
+    if (!out) return fail(GOL_EINVAL, "null out");
+    *out = gol_plan_summary{};
+    gol_status st = check_cfg(cfg);
+    if (st != GOL_OK) return st;
+    if (h == 0 || w == 0) return fail(GOL_EINVAL, "h and w must be >= 1");
+    if (h > (1ull << 40) || w > (1ull << 40)) return fail(GOL_EINVAL, "field too large");
+    if (cus <= 0 || occ_classic <= 0 || occ_hand < 0)
+        return fail(GOL_EINVAL, "cus and occ_classic must be >= 1, occ_hand >= 0");
+    if (nranks > 1 && cfg->semantics != GOL_SEM_GLOBAL)
+        return fail(GOL_EINVAL, "rank engines implement GLOBAL semantics only");
+    RankGeom g;
+    gol_config c = *cfg;
+    if (nranks > 1) {
+        st = rank_geometry(h, cfg, rank, nranks, &g);
+        if (st != GOL_OK) return st;
+        c.resident = 1;
+        c.tb_depth = g.K;
+    } else if (nranks != 1 || rank != 0) {
+        return fail(GOL_EINVAL, "rank must be 0 of 1, or 0 <= rank < nranks");
+    }
+    std::unique_ptr<gol_engine> e(new (std::nothrow) gol_engine());
+    if (!e) return fail(GOL_ENOMEM, "host allocation");
+    e->model.on = true;
+    e->model.cus = cus;
+    e->model.occ_c = occ_classic;
+    e->model.occ_h = occ_hand;
+    if (nranks > 1) {
+        e->rank = rank;
+        e->nranks = nranks;
+        e->row0 = g.row0;
+        e->R = g.R;
+        e->Hx = g.Hx;
+    } else {
+        e->R = h;
+    }
+    GOL_TRY(host_layout(e.get(), h, w, &c));
+    std::vector<std::vector<SegDesc>> raw;
+    GOL_TRY(raw_regions(e.get(), h, &c, nranks > 1 ? &g : nullptr, raw));
+    GOL_TRY(build_plans(e.get(), raw));
+    if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
+    const size_t pi = nranks > 1 ? std::min<size_t>(e->plans.size() - 1, e->K - 1) : 0;
+    const auto& p = e->plans[pi];
+    out->tb_depth = e->K;
+    out->halo_depth = (uint32_t)e->Hx;
+    out->plans = (uint32_t)e->plans.size();
+    for (int a : e->plan_alias) out->distinct_plans += a < 0 ? 1u : 0u;
+    out->rows_lo = p.segs.empty() ? 0 : p.segs[0].out_lo;
+    out->rows_hi = p.segs.empty() ? 0 : p.segs.back().out_hi;
+    out->rows_per_wave = p.rows_old ? p.rows_young : p.rpw;
+    out->rows_old = p.rows_old;
+    out->units_old = p.units_old;
+    out->strips = p.groups;
+    out->lane_shift = p.lane_shift;
+    out->total_units = p.total_units;
+    out->half_units = p.pair_units;
+    for (const auto& sg : p.segs) out->blocks += sg.nblk;
+    out->handoff = (p.hand && p.multi_blk) ? 1 : 0;
+    out->tail_off = out->handoff ? gol::handoff_toff(p.rpw, (int)e->K, e->planes) : -1;
+    out->candidates = pi < e->plan_alts.size() ? (uint32_t)e->plan_alts[pi].size() : 0u;
     return GOL_OK;
 }
 
@@ -2853,6 +2987,10 @@ gol_status gol_get_timing(gol_engine* e, gol_timing* out)
             t.kernel_ms += pt.kernel_ms;
             t.cell_gens += pt.cell_gens;
             t.cell_gens_computed += pt.cell_gens_computed;
+            t.launches_issued += pt.launches_issued;
+            t.launch_rows += pt.launch_rows;
+            t.exchanges += pt.exchanges;
+            t.exchange_ms += pt.exchange_ms;
         }
         t.streams = (uint32_t)e->parts.size();
         *out = t;

@@ -74,7 +74,7 @@ struct StepArgs {
     uint32_t* flags;      // total_units words, zeroed before every launch
     int* err;
     int64_t side_slot;    // words per slot: 2 (K-1) rows x 64 lanes x NP/2 words
-    uint64_t* wlog;       // dev timing builds only (GOL_EXP & 128): 4 words per wavefront
+    uint64_t* wlog;       // dev timing builds only (GOL_EXP & 128): 8 words per wavefront
     uint32_t* prog;       // dev (GOL_EXP & 1024): per-SIMD wave progress, 2 words per SIMD
     // Edge-aligned strips and the packed half strip (engine.cpp col_layout;
     // one-segment launches of 64-lane strips).  A lane whose neighbour lane is the

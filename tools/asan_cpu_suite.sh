@@ -17,6 +17,7 @@ mkdir -p "$(dirname "$LOG")"
   echo "# libgol: $ROOT/mpi-game-of-life_amd/build/asan/libgol_asan.so"
   echo "# oracle: $ROOT/oracle/liboracle_asan.so"
   echo "# runtime: $RT"
+  echo "# instrumented: $(nm -D "$ROOT/mpi-game-of-life_amd/build/asan/libgol_asan.so" | grep -c ' U __asan_report') asan report symbols, $(nm -D "$ROOT/mpi-game-of-life_amd/build/asan/libgol_asan.so" | grep -c ' U __ubsan_handle') ubsan handlers imported by libgol_asan.so"
   echo "# ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1"
 } > "$LOG"
 GOL_LIB="$ROOT/mpi-game-of-life_amd/build/asan/libgol_asan.so" \

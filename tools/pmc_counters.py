@@ -22,8 +22,12 @@ import statistics
 
 
 def per_kernel(path, counter):
+    """Counter values per kernel name, in dispatch order."""
     out = {}
-    for r in csv.DictReader(open(path)):
+    rows = list(csv.DictReader(open(path)))
+    if rows and "Dispatch_Id" in rows[0]:
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    for r in rows:
         if r["Counter_Name"] != counter:
             continue
         k = r["Kernel_Name"]
@@ -46,7 +50,7 @@ def config_of(log):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("prof_dir")
-    p.add_argument("--out", default="profiles/r04/counters.json")
+    p.add_argument("--out", default="profiles/r05/counters.json")
     p.add_argument("--stage-rev", type=int, default=0,
                    help="stage-logic revision of the profiled build (bench.py STAGE_REV; "
                         "0 = the current one of the profiled rule)")
@@ -54,6 +58,12 @@ def main():
     d = a.prof_dir
     cfg = config_of(os.path.join(d, "pmc_FETCH_SIZE.log"))
     n, S = cfg["size"], cfg["streams"]
+    # rows the digest reads and init_random writes: the field, or a rank engine's
+    # own rows (profile_run.py --ranks)
+    own = cfg.get("own_rows", n)
+    # (r05) only the profiled step's launches (the last `launches` of the stencil
+    # kernel): the autotuner's candidates at create are other plans
+    last = int(cfg.get("launches", 0)) or None
     kern = cfg.get("kernel", "life_tb_kernel")
     gpl = cfg.get("gens_per_launch", cfg["tb_depth"])
     fetch = per_kernel(os.path.join(d, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE")
@@ -61,10 +71,11 @@ def main():
     wq = (n + 63) // 64
     stride = (wq + 7) // 8 * 8
     # a composite engine runs digest / init per part, over 1/S of the rows each
-    f_read = n * wq * 8 / S / (statistics.mean(fetch["digest_kernel"]) * 1024)
-    f_write = n * stride * 8 / S / (statistics.mean(write["init_random_kernel"]) * 1024)
-    rd = statistics.mean(fetch[kern]) * 1024 * f_read
-    wr = statistics.mean(write[kern]) * 1024 * f_write
+    f_read = own * wq * 8 / S / (statistics.mean(fetch["digest_kernel"]) * 1024)
+    # (the user's init_random, the last one: the autotuner's fills the whole buffer)
+    f_write = own * stride * 8 / S / (statistics.mean(write["init_random_kernel"][-S:]) * 1024)
+    rd = statistics.mean(fetch[kern][-last:] if last else fetch[kern]) * 1024 * f_read
+    wr = statistics.mean(write[kern][-last:] if last else write[kern]) * 1024 * f_write
     sq = os.path.join(d, "pmc_sq", "pmc_counter_collection.csv")
     rec = dict(cfg)
     for k in ("launches", "digest0", "digest", "gens_per_launch"):
@@ -72,7 +83,7 @@ def main():
     rec.update({
         "hbm_bytes_per_launch": round(rd + wr), "read_bytes_per_launch": round(rd),
         "write_bytes_per_launch": round(wr),
-        "bytes_per_cell_gen_measured": round((rd + wr) * S / (n * n * gpl), 5),
+        "bytes_per_cell_gen_measured": round((rd + wr) * S / (own * n * gpl), 5),
         "gens_per_launch": gpl,
         "fetch_size_calibration": round(f_read, 4), "write_size_calibration": round(f_write, 4),
     })
@@ -80,10 +91,13 @@ def main():
         for c in ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
                   "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE", "SQ_INSTS_SALU"):
             v = per_kernel(sq, c).get(kern)
+            if v and last:
+                v = v[-last:]
             if v:
                 rec[c.lower() + "_per_launch"] = round(statistics.mean(v))
         rec["insts_valu_per_launch"] = rec.get("sq_insts_valu_per_launch")
-        rec["launches_profiled"] = len(per_kernel(sq, "SQ_INSTS_VALU").get(kern, []))
+        rec["launches_profiled"] = min(len(per_kernel(sq, "SQ_INSTS_VALU").get(kern, [])),
+                                       last or 1 << 30)
     stats = glob.glob(os.path.join(d, "trace", "*kernel_stats.csv"))
     if stats:  # the bench command's kernel trace: the dominant stencil instantiation
         rows = [r for r in csv.DictReader(open(stats[0])) if kern in r["Name"]]

@@ -30,13 +30,22 @@ p.add_argument("--rows-per-wave", type=int, default=0)
 p.add_argument("--handoff", type=int, default=0)
 p.add_argument("--streams", type=int, default=0)
 p.add_argument("--launches", type=int, default=16)
+p.add_argument("--ranks", type=int, default=1,
+               help="> 1: the middle rank (N // 2) of the N-way row-stripe split as one rank "
+                    "engine over an RCCL self-loop communicator (GOL_DEV_RCCL_SELF=1; its "
+                    "launches are the N-GPU run's per-rank launches, tools/rank_proxy.py)")
 p.add_argument("--gens", type=int, default=1000,
                help="resident engines: generations per launch (one launch per gol_step)")
 a = p.parse_args()
 pkg = entry.load_package()
 rule = pkg.REF_RULE if a.rule == "ref" else pkg.CONWAY
-e = pkg.Engine(a.size, a.size, rule=rule, device=0, tb_depth=a.tb_depth,
-               rows_per_wave=a.rows_per_wave, handoff=a.handoff, streams=a.streams)
+kw = dict(rule=rule, device=0, tb_depth=a.tb_depth, rows_per_wave=a.rows_per_wave,
+          handoff=a.handoff)
+if a.ranks > 1:
+    os.environ["GOL_DEV_RCCL_SELF"] = "1"
+    e = pkg.Engine(a.size, a.size, rank=a.ranks // 2, nranks=a.ranks, uid=pkg.unique_id(), **kw)
+else:
+    e = pkg.Engine(a.size, a.size, streams=a.streams, **kw)
 e.init_random(1)
 d0 = e.digest()
 e.set_timing(1)
@@ -50,7 +59,9 @@ else:
 e.sync()
 tm = e.timing()
 print(json.dumps({"size": a.size, "rule": a.rule, "tb_depth": e.tb_depth,
-                  "streams": max(1, tm["streams"]), "n_gpus": 1,
+                  "streams": max(1, tm["streams"]), "n_gpus": a.ranks,
+                  "own_rows": e.rows, "halo_depth": e.halo_depth,
+                  "rows_per_launch": round(tm["launch_rows"] / max(1, tm["launches"]), 1),
                   "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
                   "kernel": "life_res_kernel" if e.resident else "life_tb_kernel",
                   "gens_per_launch": gens_per_launch,

@@ -3,7 +3,7 @@
 GOL_EXP & 128, tools/exp_build.sh), and the wall-clock rate of the same shape.
 
 Each wavefront logs its s_memrealtime start/end stamps (100 MHz), HW_ID and
-XCC_ID.  Wavefronts sharing a SIMD (same XCC, SE, SH, CU, SIMD) are paired, and
+XCC_ID, and (r05) the stamps where its warm-up and its steady blocks end.  Wavefronts sharing a SIMD (same XCC, SE, SH, CU, SIMD) are paired, and
 the tool reports how long the first-finishing wave of a pair ends before the
 second (the time its partner runs alone on the SIMD), the spread of start and
 end stamps, and the launch span.
@@ -48,13 +48,13 @@ def main():
         e.sync()
         ts.append(time.perf_counter() - t0)
     tcups = a.rows * a.width * a.gens / statistics.median(ts) / 1e12
-    log = torch.zeros(4 * 65536, dtype=torch.int64, device="cuda")
+    log = torch.zeros(8 * 65536, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
     L.gol_dev_set_wave_log(ctypes.c_void_p(log.data_ptr()))
     e.step(e.tb_depth)  # one full-depth launch
     e.sync()
     L.gol_dev_set_wave_log(ctypes.c_void_p(0))
-    w = log.view(-1, 4).cpu().numpy().astype("uint64")
+    w = log.view(-1, 8).cpu().numpy().astype("uint64")
     w = w[w[:, 0] != 0]
     start, end = w[:, 0].astype("int64"), w[:, 1].astype("int64")
     hw = [int(x) for x in w[:, 2]]
@@ -120,6 +120,28 @@ def main():
         ends = [float(end[i] - t0) / 100.0 for i, s in enumerate(slot) if s == sl]
         if ends:
             rec[f"slot{sl}_end_us_median"] = round(statistics.median(ends), 2)
+    # (r05) phases of each wavefront: warm-up (the unrolled first 2K steps), steady
+    # blocks, tail (hand-off side rows / classic drain), by block length
+    tw, tsd = w[:, 4].astype("int64"), w[:, 5].astype("int64")
+    nrows = (w[:, 6] & 0xFFFFFFFF).astype("int64")
+    tb1 = (w[:, 6] >> 32).astype("int64")  # second warm-up block's end, from the start
+    tb0 = w[:, 7].astype("int64")
+    by_len = collections.defaultdict(list)
+    for i in range(len(w)):
+        if tw[i] and tsd[i]:
+            by_len[int(nrows[i])].append(((tw[i] - start[i]) / 100.0, (tsd[i] - tw[i]) / 100.0,
+                                          (end[i] - tsd[i]) / 100.0,
+                                          (tb0[i] - start[i]) / 100.0 if tb0[i] else 0.0,
+                                          (start[i] - t0) / 100.0, tb1[i] / 100.0))
+    rec["phases_us_by_rows"] = {
+        str(k): {"waves": len(v),
+                 "warm": round(statistics.median(x[0] for x in v), 2),
+                 "steady": round(statistics.median(x[1] for x in v), 2),
+                 "tail": round(statistics.median(x[2] for x in v), 2),
+                 "first_block": round(statistics.median(x[3] for x in v), 2),
+                 "second_block": round(statistics.median(x[5] for x in v), 2),
+                 "start_offset": round(statistics.median(x[4] for x in v), 2)}
+        for k, v in sorted(by_len.items(), key=lambda kv: -len(kv[1]))[:6]}
     print(json.dumps(rec), flush=True)
     e.close()
 
