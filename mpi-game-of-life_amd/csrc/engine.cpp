@@ -1647,6 +1647,10 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     a.out = e->buf[e->cur ^ 1];
     a.segs = p.dev;
     a.nseg = (int32_t)p.segs.size() + (p.pair_units ? 1 : 0);
+    if (p.segs.size() == 1) {
+        a.seg0_only = 1;
+        a.seg0 = p.segs[0];
+    }
     a.strips = p.groups;
     a.lane_shift = p.lane_shift;
     a.stride = (int64_t)e->stride;

@@ -89,6 +89,10 @@ struct StepArgs {
     // that no unit of theirs is a hand-off producer or consumer); pairs holds
     // (first row A, first row B or -1 for lanes 32-63 idle, rows) per unit.
     int32_t edge;
+    // (r05) the launch's one segment (nseg is 1, or 2 with the half strip's
+    // copy): the kernel takes it from here instead of the device table
+    int32_t seg0_only;
+    SegDesc seg0;
     int64_t right_q0;
     int64_t half_q0, half_hi;
     int64_t pair0, pair_units;

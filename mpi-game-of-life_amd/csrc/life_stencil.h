@@ -456,6 +456,10 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 #ifndef GOL_EXP
 #define GOL_EXP 0
 #endif
+// (r05) warm-up rows loaded up front (see the kernel); 0 = the r04 one-block ring
+#ifndef GOL_WARM_PREFETCH
+#define GOL_WARM_PREFETCH 1
+#endif
 
 template <int K, int RULE, int NP, bool HAND, int TOFF>
 // (capped at 256 registers to keep 2 waves per SIMD: the 8-step-prefetch hand-off
@@ -511,13 +515,31 @@ void life_tb_kernel(StepArgs a)
     uint32_t prog_n = 0, prog_m = 0;
 #endif
 
-    int sidx = 0;
-    for (int j = 1; j < a.nseg; ++j)
-        if (unit >= a.segs[j].unit0) sidx = j;
-    const SegDesc sg = a.segs[sidx];
-    const int64_t u = unit - sg.unit0;
     // a unit of the packed half strip (uniform): its two row blocks from the table
     const bool pu = a.pair_units > 0 && unit >= a.pair0;
+    // (r05) One-segment launches (every launch of a GLOBAL or rank engine) take
+    // their segment from the kernel arguments, which arrive with the first scalar
+    // loads, instead of a dependent table walk in memory at every wavefront's
+    // start; the half strip's units use it with one block from pair0 (the device
+    // table's extra segment, engine.cpp build_plans).
+    SegDesc sg;
+    if (a.seg0_only) {
+        sg = a.seg0;
+        if (pu) {
+            sg.nblk = 1;
+            sg.unit0 = a.pair0;
+        }
+    } else {
+        int sidx = 0;
+        for (int j = 1; j < a.nseg; ++j)
+            if (unit >= a.segs[j].unit0) sidx = j;
+        sg = a.segs[sidx];
+    }
+    const int64_t u = unit - sg.unit0;
+    // strip and block-from-the-bottom of the unit: 32-bit (units < 2^31; the 64-bit
+    // division is a long VALU/SALU sequence in every wavefront's prologue)
+    const uint32_t u_blk = (uint32_t)u / (uint32_t)a.strips;
+    const int64_t u_strip = (int64_t)((uint32_t)u - u_blk * (uint32_t)a.strips);
     int64_t pair_a = 0, pair_b = -1, pair_len = 0;
     if (pu) {
         // (row indices < 2^31; readfirstlane keeps them, and every row bound derived
@@ -528,7 +550,7 @@ void life_tb_kernel(StepArgs a)
         pair_len = __builtin_amdgcn_readfirstlane((int32_t)pd[2]);
     }
     // row blocks bottom-up: the block below (a hand-off producer) has the smaller index
-    const int64_t blk = pu ? 0 : sg.nblk - 1 - u / a.strips;
+    const int64_t blk = pu ? 0 : sg.nblk - 1 - (int64_t)u_blk;
     // strip `strip` of the row block lives in lanes [sub*L, sub*L + L); the DPP
     // shifts cross from one strip into the next only at halo lanes
     const int lshift = a.lane_shift;
@@ -547,14 +569,14 @@ void life_tb_kernel(StepArgs a)
         exact = hl >= 1 && q <= a.half_hi;
         on = lane < 32 || pair_b >= 0;
     } else if (a.edge) {
-        const int64_t s = u % a.strips;
+        const int64_t s = u_strip;
         qfirst = s == 0 ? 0 : (s == a.strips - 1 && a.right_q0 >= 0) ? a.right_q0 : 62 * s;
         q = qfirst + lane;
         exact = (lane >= 1 || q == 0) && (lane <= 62 || q == a.ng - 1);
     } else {
         // q = qbase + sub*(L-2) + lin, qbase (uniform) the group one left of the
         // wave's first strip
-        const int64_t qbase = (u % a.strips) * (int64_t)(1 << lshift) * (L - 2) - 1;
+        const int64_t qbase = u_strip * (int64_t)(1 << lshift) * (L - 2) - 1;
         qfirst = qbase + 1;
         q = qbase + sub * (L - 2) + lin;
         exact = lin >= 1 && lin <= L - 2;
@@ -585,8 +607,10 @@ void life_tb_kernel(StepArgs a)
     int64_t rb = pu ? pair_a : sg.out_lo + blk * a.rows_per_wave;
     int64_t rlen = pu ? pair_len : a.rows_per_wave;
     if (a.rows_old && !pu) {
-        const int64_t s = u % a.strips;
-        const int64_t jo = min(sg.nblk, max((int64_t)0, (a.units_old - s + a.strips - 1) / a.strips));
+        const int32_t s = (int32_t)u_strip;
+        const int64_t jo = min(sg.nblk, (int64_t)(a.units_old > s ? (uint32_t)(a.units_old - s + a.strips - 1) /
+                                                                       (uint32_t)a.strips
+                                                                 : 0u));
         const int64_t ny = sg.nblk - jo;  // young blocks, on top
         if (blk >= ny) {
             rb = sg.out_lo + ny * a.rows_per_wave + (blk - ny) * a.rows_old;
@@ -641,8 +665,29 @@ void life_tb_kernel(StepArgs a)
         return load_grp<NP>(reinterpret_cast<const uint64_t*>(base + (in ? voff : voff_side)));
     };
     Grp<NP> ring[kPrefetch];
+#if GOL_WARM_PREFETCH
+    // (r05) Every row of the unrolled warm-up is loaded up front, and the steady
+    // ring two warm-up blocks before the steady loop.  With the one-block ring
+    // the compiler pulled each warm-up block's ingest up into the block before
+    // (no scheduling barriers there), so every refill was consumed right after
+    // its issue: a chain of HBM round trips (s_waitcnt vmcnt(0/1) after each
+    // load) that made the 2K warm-up steps take 16-20 us per wavefront at every
+    // shape (profiles/r05/wave_phases_*.jsonl).
+    Grp<NP> wring[kWarmSteps];
+#pragma unroll
+    for (int p = 0; p < kWarmSteps; ++p) wring[p] = load_step(p);
+    constexpr int kSteadyIssue = kWarmSteps >= 2 * kPrefetch ? kWarmSteps - 2 * kPrefetch : 0;
+#else
 #pragma unroll
     for (int p = 0; p < kPrefetch; ++p) ring[p] = load_step(p);
+#endif
+#if GOL_EXP & 16384
+    // dev probe of a wavefront's start (tools/wave_log.py --probe): the initial
+    // loads issued, and all of them landed (results stay valid, timing does not)
+    const uint64_t wl_pi = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t wl_pl = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // row of step t: an input row is dead outside the field / buffer; a side row
     // comes as the block below computed it; columns >= w masked.  SIDE: the step
@@ -768,6 +813,15 @@ void life_tb_kernel(StepArgs a)
         // births masked everywhere but in kPure blocks (t_plain_end)
         constexpr bool kMask = kBirths && kMode != kPure;
         Pl<NP> x[kPrefetch];
+#if GOL_WARM_PREFETCH
+        if constexpr (kGuard) {
+#pragma unroll
+            for (int p = 0; p < kPrefetch; ++p) {
+                x[p] = ingest(t0 + p, wring[t0 + p], std::false_type{});
+                if (t0 == kSteadyIssue) ring[p] = load_in(kWarmSteps + p);
+            }
+        } else
+#endif
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
             x[p] = ingest(t0 + p, ring[p], std::integral_constant<bool, kSideMode>{});
@@ -855,8 +909,22 @@ void life_tb_kernel(StepArgs a)
     // Warm-up blocks, unrolled (compile-time guards).
     constexpr int kWarm = kWarmSteps;
     static_assert(!HAND || kWarm >= 2 * K, "side rows are all stored in the warm-up blocks");
+#if GOL_EXP & 128
+    uint64_t wl_tb = 0, wl_tb1 = 0;  // after the first / second warm-up block
+#pragma unroll
+    for (int t0 = 0; t0 < kWarm; t0 += kPrefetch) {
+        block(t0, std::integral_constant<int, kWarmBlk>{});
+        if (t0 == 0) wl_tb = __builtin_amdgcn_s_memrealtime();
+        if (t0 == kPrefetch) wl_tb1 = __builtin_amdgcn_s_memrealtime();
+    }
+#else
 #pragma unroll
     for (int t0 = 0; t0 < kWarm; t0 += kPrefetch) block(t0, std::integral_constant<int, kWarmBlk>{});
+#endif
+#if GOL_EXP & 128
+    // phase stamps (r05): issue time of the warm-up's end and the steady blocks' end
+    const uint64_t wl_tw = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // Steady state: whole blocks of input steps.  A consumer stops TOFF steps
     // before t_side; its last whole block's refill is the first to reach t_side.
@@ -887,6 +955,9 @@ void life_tb_kernel(StepArgs a)
     // a producer whose stream had no steady block (a short last block) signals here
     if constexpr (HAND)
         if (producer && T <= kWarm && !(GOL_EXP & 2)) signal();
+#if GOL_EXP & 128
+    const uint64_t wl_ts = __builtin_amdgcn_s_memrealtime();
+#endif
 
     if constexpr (HAND && !(GOL_EXP & 8)) {
         if (consumer) {
@@ -944,7 +1015,18 @@ void life_tb_kernel(StepArgs a)
     }
 #if GOL_EXP & 128
     if (a.wlog && lane == 0) {
-        uint64_t* wl = a.wlog + unit * 4;
+        // 8 words per wavefront: start, end, HW_ID | XCC_ID, block | workgroup,
+        // warm-up end, steady end (tools/wave_log.py)
+        uint64_t* wl = a.wlog + unit * 8;
+#if GOL_EXP & 16384
+        wl[4] = wl_pi;
+        wl[5] = wl_pl;
+#else
+        wl[4] = wl_tw;
+        wl[5] = wl_ts;
+#endif
+        wl[6] = (uint64_t)(re - rb) | ((wl_tb1 - wl_t0) << 32);
+        wl[7] = wl_tb;
         wl[0] = wl_t0;
         wl[1] = __builtin_amdgcn_s_memrealtime();
         wl[2] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) |

@@ -33,6 +33,9 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--tag", default="")
     p.add_argument("--cus", type=int, default=256)
+    p.add_argument("--probe", action="store_true",
+                   help="GOL_EXP & 16384 builds: words 4/5 are the start probe (initial loads "
+                        "issued / landed) instead of the warm-up / steady ends")
     a = p.parse_args()
     import torch
     pkg = entry.load_package()
@@ -133,11 +136,12 @@ def main():
                                           (end[i] - tsd[i]) / 100.0,
                                           (tb0[i] - start[i]) / 100.0 if tb0[i] else 0.0,
                                           (start[i] - t0) / 100.0, tb1[i] / 100.0))
+    names = ("to_loads_issued", "loads_landed", "to_end") if a.probe else ("warm", "steady", "tail")
     rec["phases_us_by_rows"] = {
         str(k): {"waves": len(v),
-                 "warm": round(statistics.median(x[0] for x in v), 2),
-                 "steady": round(statistics.median(x[1] for x in v), 2),
-                 "tail": round(statistics.median(x[2] for x in v), 2),
+                 names[0]: round(statistics.median(x[0] for x in v), 2),
+                 names[1]: round(statistics.median(x[1] for x in v), 2),
+                 names[2]: round(statistics.median(x[2] for x in v), 2),
                  "first_block": round(statistics.median(x[3] for x in v), 2),
                  "second_block": round(statistics.median(x[5] for x in v), 2),
                  "start_offset": round(statistics.median(x[4] for x in v), 2)}
