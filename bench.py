@@ -236,7 +236,7 @@ def ctl_device(dist):
     return "cpu" if dist.get_backend() == "gloo" else "cuda"
 
 
-def rccl_selfcheck(pkg, dist, torch, world, rank, local):
+def rccl_selfcheck(pkg, dist, torch, world, rank, local, handoff=0):
     """N > 1: the RCCL halo path end to end on a small field before the timed run.
     Every rank advances its stripe of a 4096^2 B3/S23 field (rounds of Hx
     generations with ncclSend/Recv exchanges); rank 0 evolves the whole field
@@ -250,7 +250,7 @@ def rccl_selfcheck(pkg, dist, torch, world, rank, local):
     uid = [pkg.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     with pkg.Engine(n, n, rule=pkg.CONWAY, device=local, rank=rank, nranks=world,
-                    uid=uid[0]) as e:
+                    uid=uid[0], handoff=handoff) as e:
         hx = e.halo_depth
         row0, rows = e.row0, e.rows
         try:
@@ -269,7 +269,7 @@ def rccl_selfcheck(pkg, dist, torch, world, rank, local):
     rec = {"field": f"{n}x{n}", "rule": "B3/S23", "generations": gens, "halo_depth": hx,
            "ranks": world}
     if rank == 0:
-        with pkg.Engine(n, n, rule=pkg.CONWAY, device=local) as ref:
+        with pkg.Engine(n, n, rule=pkg.CONWAY, device=local, handoff=handoff) as ref:
             ref.init_random(seed)
             ref.step(gens)
             want = ref.digest()
@@ -402,6 +402,13 @@ def main():
     torch.cuda.set_device(local)
     kw = dict(rule=rule, device=local, tb_depth=a.tb_depth, rows_per_wave=a.rows_per_wave,
               handoff=a.handoff)
+    # ranks sharing a GPU (the one-GPU rehearsal) must not run kernels that wait for
+    # other wavefronts of their own launch: two such launches from two processes can
+    # hold each other's slots (the per-process registry cannot see the other
+    # process).  Classic blocks there, as gol-mpi does when ranks share a GPU.
+    shared_gpu = rehearsal and world > max(1, torch.cuda.device_count())
+    if shared_gpu and not a.handoff:
+        kw["handoff"] = 1
 
     def barrier():
         if world > 1:
@@ -423,7 +430,7 @@ def main():
     modes = None
     if world > 1:
         dist.init_process_group("gloo" if rehearsal else "nccl")
-        selfcheck = rccl_selfcheck(pkg, dist, torch, world, rank, local)
+        selfcheck = rccl_selfcheck(pkg, dist, torch, world, rank, local, kw["handoff"])
         # the overlapped exchange (band launch + RCCL exchange on a side stream
         # beside the interior launch, exchange_overlap = 2) against the default
         # blocking one: the same K steps, reported beside `value`
@@ -591,6 +598,7 @@ def main():
         }
         if rehearsal:
             rec["rehearsal"] = True
+            rec["rehearsal_classic_blocks"] = shared_gpu
             rec["rehearsal_value"] = round(gcups, 2)
             rec["physical_gpus"] = torch.cuda.device_count()
         if world == 1 and not a.no_cpu_baseline:

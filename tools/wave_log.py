@@ -146,6 +146,34 @@ def main():
                  "second_block": round(statistics.median(x[5] for x in v), 2),
                  "start_offset": round(statistics.median(x[4] for x in v), 2)}
         for k, v in sorted(by_len.items(), key=lambda kv: -len(kv[1]))[:6]}
+    # (r05) the last-finishing waves, which set the launch's end: their age class
+    # (slot), block index from the bottom, strip, row count, XCC, and start offset
+    order = sorted(range(len(w)), key=lambda i: -int(end[i]))
+    blkv = (w[:, 3] & 0xFFFFFFFF).astype("int64")
+    n_last = max(1, len(w) // 50)
+    last = order[:n_last]
+    rec["last_2pct"] = {
+        "end_us_min": round(float(end[last[-1]] - t0) / 100.0, 2),
+        "slot": dict(collections.Counter(int(hw[i]) & 15 for i in last)),
+        "xcc": dict(collections.Counter(int(hw[i]) >> 32 for i in last)),
+        "rows": dict(collections.Counter(int(nrows[i]) for i in last)),
+        "blk": dict(collections.Counter(int(blkv[i]) for i in last).most_common(8)),
+        "start_us_median": round(statistics.median(float(start[i] - t0) / 100.0 for i in last), 2),
+        "dur_us_median": round(statistics.median(float(dur_us[i]) for i in last), 2),
+        "wg": sorted(int(wg[i]) for i in last)[:24],
+    }
+    # (r05) per XCC (HW_REG_XCC_ID): wavefronts, median / max end and median duration
+    # of the old (slot 0) and young (slot 1) waves
+    by_x = collections.defaultdict(list)
+    for i in range(len(w)):
+        by_x[int(hw[i]) >> 32].append(i)
+    rec["per_xcc"] = {
+        str(x): {"waves": len(v),
+                 "end_med": round(statistics.median(float(end[i] - t0) for i in v) / 100.0, 2),
+                 "end_max": round(max(float(end[i] - t0) for i in v) / 100.0, 2),
+                 "dur_old": round(statistics.median([float(dur_us[i]) for i in v if int(hw[i]) & 15 == 0] or [0]), 2),
+                 "dur_young": round(statistics.median([float(dur_us[i]) for i in v if int(hw[i]) & 15 == 1] or [0]), 2)}
+        for x, v in sorted(by_x.items())}
     print(json.dumps(rec), flush=True)
     e.close()
 
