@@ -147,6 +147,35 @@ __device__ __forceinline__ Grp<NP> load_grp(const uint64_t* p)
                                    __HIP_MEMORY_SCOPE_AGENT);
     return g;
 }
+// Field rows (written by an earlier launch, so plain loads would see them too).
+// Dev A/B (GOL_NT_LOADS=1): non-temporal loads (global_load ... nt).  A launch's
+// start needs every wavefront's first rows at once, and with the field larger
+// than the 256 MB Infinity Cache (65536^2) allocating loads took 12.8 us to
+// deliver 32 rows to every wavefront against 4.9 us for nt loads
+// (tools/burst_probe.hip, profiles/r05/burst_probe.jsonl).  In the kernel they
+// lost: 65536^2 156.7-156.9 vs 158.0-158.3 TCUPS, the 8-way rank 107.5-107.9 vs
+// 117.4-118.3 (the rows a block shares with its neighbours -- halo lanes of the
+// strips beside it, the rows around a block seam -- are no longer kept in L2);
+// nt stores beside them 111.6-111.7 (profiles/r05/ab_nt_loads_stores_rejected.jsonl).
+#ifndef GOL_NT_LOADS
+#define GOL_NT_LOADS 0
+#endif
+#ifndef GOL_NT_STORES
+#define GOL_NT_STORES 0
+#endif
+template <int NP>
+__device__ __forceinline__ Grp<NP> load_field(const uint64_t* p)
+{
+#if GOL_NT_LOADS
+    Grp<NP> g;
+#pragma unroll
+    for (int i = 0; i < NP / 2; ++i) g.w[i] = __builtin_nontemporal_load(p + i);
+    return g;
+#else
+    return load_grp<NP>(p);
+#endif
+}
+
 template <int NP>
 __device__ __forceinline__ void store_side(uint64_t* p, const Pl<NP>& x)
 {
@@ -658,11 +687,12 @@ void life_tb_kernel(StepArgs a)
     // step t_side on the block below's side row s - t_side (uniform select)
     auto load_step = [&](int32_t s) -> Grp<NP> {
         if constexpr (!HAND)
-            return load_grp<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
-        const bool in = s < t_side;
-        const char* base = in ? in_rows + (int64_t)s * row_bytes
-                              : dn_side + (int64_t)(s - t_side) * kSideRowBytes;
-        return load_grp<NP>(reinterpret_cast<const uint64_t*>(base + (in ? voff : voff_side)));
+            return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
+        if (s < t_side)
+            return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
+        // side rows: stored sc1 by another wavefront of this launch, loaded sc1
+        return load_grp<NP>(reinterpret_cast<const uint64_t*>(
+            dn_side + (int64_t)(s - t_side) * kSideRowBytes + voff_side));
     };
     Grp<NP> ring[kPrefetch];
 #if GOL_WARM_PREFETCH
@@ -675,7 +705,8 @@ void life_tb_kernel(StepArgs a)
     // shape (profiles/r05/wave_phases_*.jsonl).
     Grp<NP> wring[kWarmSteps];
 #pragma unroll
-    for (int p = 0; p < kWarmSteps; ++p) wring[p] = load_step(p);
+    for (int p = 0; p < kWarmSteps; ++p)  // (input rows: t_side >= warm-up + 2 blocks)
+        wring[p] = load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)p * row_bytes + voff));
     constexpr int kSteadyIssue = kWarmSteps >= 2 * kPrefetch ? kWarmSteps - 2 * kPrefetch : 0;
 #else
 #pragma unroll
@@ -700,7 +731,7 @@ void life_tb_kernel(StepArgs a)
         return x;
     };
     auto load_in = [&](int32_t s) -> Grp<NP> {
-        return load_grp<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
+        return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
     };
     // stage g (generation g+1) at step t: emits local row row_first + t - (g+1)
     // With births (rules other than B/S2) nothing may come alive outside the field:
@@ -748,9 +779,17 @@ void life_tb_kernel(StepArgs a)
 #endif
     }
     auto store = [&](int32_t t, const Pl<NP>& x) {
-        if (t >= 2 * K && t < T && st_lane)
+        if (t >= 2 * K && t < T && st_lane) {
+#if GOL_NT_STORES
+            const Grp<NP> g = words_of(x);
+            uint64_t* o = reinterpret_cast<uint64_t*>(out_rows + (int64_t)(t - 2 * K) * row_bytes + voff);
+#pragma unroll
+            for (int i = 0; i < NP / 2; ++i) __builtin_nontemporal_store(g.w[i], o + i);
+#else
             *reinterpret_cast<Grp<NP>*>(out_rows + (int64_t)(t - 2 * K) * row_bytes + voff) =
                 words_of(x);
+#endif
+        }
     };
 
     // Hand-off signalling (HAND kernels), done in steady blocks after the compute:
