@@ -230,6 +230,11 @@ gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint3
  * the models' plan (0 when nothing was timed).  Out pointers may be NULL. */
 gol_status gol_plan_tuning(gol_engine* e, uint32_t* variant, float* tuned_us, float* model_us);
 
+/* Passes per full-depth launch of the first full-depth plan: 1, or 2-3 for
+ * multi-pass launches (each launch runs that many depth-K passes over its row
+ * blocks, alternating direction; dev switch GOL_DEV_PASSES at create). */
+gol_status gol_plan_passes(gol_engine* e, uint32_t* passes);
+
 /* gol_digest restricted to field rows [row0, row0 + rows) (for a rank engine:
  * the part of its own rows inside that range).  Lets one engine of the whole
  * field check each rank's stripe separately. */

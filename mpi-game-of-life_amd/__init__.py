@@ -35,7 +35,7 @@ EXPORTS = [
     "gol_create_rank", "gol_create_group", "gol_group_step", "gol_plan_info",
     "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
     "gol_plan_resident", "gol_plan_skew", "gol_plan_columns", "gol_plan_tuning",
-    "gol_digest_rows", "gol_comm_info", "gol_plan_model",
+    "gol_digest_rows", "gol_comm_info", "gol_plan_model", "gol_plan_passes",
 ]
 
 # gol_plan_tuning's variants (engine.cpp kTuneVariantNames): 0 = the models' plan
@@ -179,6 +179,7 @@ def lib():
                                             ctypes.POINTER(Transport), ctypes.POINTER(vp)]
     pf32 = ctypes.POINTER(ctypes.c_float)
     L.gol_plan_tuning.argtypes = [vp, ctypes.POINTER(u32), pf32, pf32]
+    L.gol_plan_passes.argtypes = [vp, ctypes.POINTER(u32)]
     L.gol_digest_rows.argtypes = [vp, u64, u64, pu64, pu64]
     pi32 = ctypes.POINTER(ctypes.c_int)
     L.gol_comm_info.argtypes = [vp, pi32, pi32, pi32, pi32, pi32]
@@ -194,7 +195,7 @@ def lib():
                  "gol_create_group", "gol_group_step", "gol_plan_info", "gol_plan_handoff",
                  "gol_plan_resident", "gol_plan_skew", "gol_plan_columns",
                  "gol_create_rank_transport", "gol_round_schedule", "gol_plan_tuning",
-                 "gol_digest_rows", "gol_comm_info", "gol_plan_model"]:
+                 "gol_digest_rows", "gol_comm_info", "gol_plan_model", "gol_plan_passes"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -332,6 +333,9 @@ class Engine:
         # of the plan that runs, of the models' plan); us 0 = not timed
         self.tuning = (TUNE_VARIANTS[tv.value] if tv.value < len(TUNE_VARIANTS) else str(tv.value),
                        round(tu.value, 2), round(mu.value, 2))
+        np_ = ctypes.c_uint32()
+        _check(lib().gol_plan_passes(self._h, ctypes.byref(np_)))
+        self.passes = np_.value  # passes per full-depth launch (multi-pass launches)
 
     def close(self):
         if self._h:

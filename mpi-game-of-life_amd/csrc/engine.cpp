@@ -223,9 +223,16 @@ struct gol_engine {
     std::vector<gol_engine*> parts;
 
     uint64_t buf_rows = 0;
-    uint64_t* alloc[2] = {nullptr, nullptr};
-    uint64_t* buf[2] = {nullptr, nullptr};
+    // state buffers: 2, or 4 with multi-pass launches (a launch of P <= 3 passes
+    // reads buf[cur] and writes buf[cur + 1 .. cur + P], mod nbuf); those also hold
+    // a shadow half (shadow_off bytes after each row) for the strips' halo lanes
+    uint64_t* alloc[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t* buf[4] = {nullptr, nullptr, nullptr, nullptr};
     int cur = 0;
+    int nbuf = 2;
+    uint32_t npass = 1;       // passes per full-depth launch the engine may run
+    uint32_t shadow_off = 0;  // bytes from a buffer word to its shadow
+    uint32_t* mpflags = nullptr;  // multi-pass head/done flags: 4 x max units
 
     // plans: plan p = a device table of nseg SegDesc (+ host copy)
     struct Plan {
@@ -252,6 +259,9 @@ struct gol_engine {
         // a copy of an earlier plan of the same rows (rank engines: the full-depth
         // launches of a round share one plan); its device tables are the owner's
         bool alias = false;
+        // passes per full-depth launch of this plan (multi-pass launches, life_stencil.h:
+        // one-segment plans of one round without the half strip; 1 = single pass)
+        int32_t npass = 1;
         // autotuner: the candidate that runs (0 = the models' plan, else 1 + the
         // index in kTuneVariantNames) and its best create-time launch vs the
         // models' plan (ms; 0 = not tuned)
@@ -705,13 +715,22 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
                     ? gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, true)
                     : 0;
     }
+    // occupancy of the multi-pass kernels (their register use may differ)
+    int occ_mp_c = occ_c, occ_mp_h = occ_h;
+    if (e->npass > 1 && !e->model.on) {
+        occ_mp_c = gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, false, true);
+        occ_mp_h = occ_h ? gol::life_blocks_per_cu((int)e->K, e->rule, e->planes, true, true) : 0;
+    }
     int64_t max_units = 0;
-    bool any_hand = false;
+    bool any_hand = false, any_mp = false;
     // the packed half strip of one-segment plans (col_layout; GOL_DEV_PAIRS=0 turns
     // it off for A/B): the planners count its units
     // (the kernel reads the half strip's row numbers as 32-bit: buffers up to 2^30 rows)
     const char* dev_pairs = std::getenv("GOL_DEV_PAIRS");
-    const int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) || e->buf_rows >= (1ull << 30)
+    // (multi-pass launches run no half strip: its pair units close their blocks
+    // the classic way and have no pass protocol)
+    const int64_t hs = (dev_pairs && std::atoi(dev_pairs) == 0) || e->buf_rows >= (1ull << 30) ||
+                               e->npass > 1
                            ? 0
                            : (int64_t)e->stride;
     auto units_of = [&](const std::vector<SegDesc>& segs, int32_t groups, int shift, int64_t R,
@@ -898,8 +917,18 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
             }
             p.own_rows += (double)std::max<int64_t>(0, ohi - olo);
         }
+        // Multi-pass launches: every wavefront waits for its row neighbours between
+        // passes, so the plan must be one round of the occupancy (all units resident)
+        {
+            const int occ = std::min(p.hand ? occ_h : occ_c, p.hand ? occ_mp_h : occ_mp_c);
+            p.npass = e->npass > 1 && !band && !inner && p.segs.size() == 1 && !p.pair_units &&
+                              p.total_units <= (int64_t)occ * slots_first
+                          ? (int32_t)e->npass
+                          : 1;
+        }
         max_units = std::max(max_units, p.total_units);
         any_hand |= p.hand && p.multi_blk;
+        any_mp |= p.npass > 1;
         if (std::getenv("GOL_DEV_PLANS"))  // dev: the launch plans as built
             std::fprintf(stderr, "plan %zu: rows [%lld, %lld) x %zu segs, R %lld, strips %d, units %lld, "
                          "hand %d, skew %d/%d, half-strip units %lld (rows %lld)\n", pi,
@@ -1010,14 +1039,20 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
     }
 #endif
     HIP_TRY(hipMemset(e->d_err, 0, sizeof(int)));
-    if (any_hand && max_units > 0) {
+    if ((any_hand || any_mp) && max_units > 0) {
+        // (multi-pass: hand-off slots and flags per pass parity)
         const size_t slot = (size_t)2 * (e->K - 1) * 64 * (size_t)(e->planes / 2);
+        const size_t par = any_mp ? 2 : 1;
         const int regions = e->overlap ? 2 : 1;
         for (int r = 0; r < regions; ++r) {
-            HIP_TRY(hipMalloc(&e->side[r], (size_t)max_units * slot * sizeof(uint64_t)));
-            HIP_TRY(hipMalloc(&e->flags[r], (size_t)max_units * sizeof(uint32_t)));
-            HIP_TRY(hipMemset(e->flags[r], 0, (size_t)max_units * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&e->side[r], par * (size_t)max_units * slot * sizeof(uint64_t)));
+            HIP_TRY(hipMalloc(&e->flags[r], par * (size_t)max_units * sizeof(uint32_t)));
+            HIP_TRY(hipMemset(e->flags[r], 0, par * (size_t)max_units * sizeof(uint32_t)));
         }
+    }
+    if (any_mp && max_units > 0) {
+        HIP_TRY(hipMalloc(&e->mpflags, 4 * (size_t)max_units * sizeof(uint32_t)));
+        HIP_TRY(hipMemset(e->mpflags, 0, 4 * (size_t)max_units * sizeof(uint32_t)));
     }
     return GOL_OK;
 }
@@ -1379,9 +1414,23 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
     GOL_TRY(raw_regions(e, h, cfg, geom, raw));
 
     const size_t words = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
-    for (int b = 0; b < 2; ++b) {
-        HIP_TRY(hipMalloc(&e->alloc[b], words * sizeof(uint64_t)));
-        HIP_TRY(hipMemsetAsync(e->alloc[b], 0, words * sizeof(uint64_t), e->stream));
+    // Multi-pass launches (GOL_DEV_PASSES = 2 or 3; life_stencil.h): single-GPU
+    // engines alone on their device and rank engines, fields whose shadow offset
+    // fits the kernel's 32-bit lane offsets, depths whose P K outer halo columns
+    // stay inside the halo lane (P K < 64)
+    if (const char* v = std::getenv("GOL_DEV_PASSES")) {
+        const int np = std::atoi(v);
+        if (np >= 2 && np <= 3 && !e->shared_device && np * (int)e->K < 64 &&
+            gol::multipass_kernel_exists((int)e->K, e->rule, e->planes) &&
+            (words + e->stride) * sizeof(uint64_t) < (1ull << 32))
+            e->npass = (uint32_t)np;
+    }
+    const size_t halves = e->npass > 1 ? 2 : 1;
+    e->nbuf = e->npass > 1 ? 4 : 2;
+    e->shadow_off = e->npass > 1 ? (uint32_t)(words * sizeof(uint64_t)) : 0u;
+    for (int b = 0; b < e->nbuf; ++b) {
+        HIP_TRY(hipMalloc(&e->alloc[b], halves * words * sizeof(uint64_t)));
+        HIP_TRY(hipMemsetAsync(e->alloc[b], 0, halves * words * sizeof(uint64_t), e->stream));
         e->buf[b] = e->alloc[b] + (size_t)gol::kGuardRows * e->stride;
     }
     HIP_TRY(hipMalloc(&e->d_acc, 2 * sizeof(unsigned long long)));
@@ -1407,9 +1456,9 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
                 r.resident++;
             } else {
                 bool hand = false;
-                for (const auto& pl : e->plans) hand |= pl.hand && pl.multi_blk;
+                for (const auto& pl : e->plans) hand |= (pl.hand && pl.multi_blk) || pl.npass > 1;
                 for (const auto& alts : e->plan_alts)
-                    for (const auto& pl : alts) hand |= pl.hand && pl.multi_blk;
+                    for (const auto& pl : alts) hand |= (pl.hand && pl.multi_blk) || pl.npass > 1;
                 if (hand && e->side[0]) {
                     e->reg_hand = true;
                     r.hand = e;
@@ -1422,7 +1471,7 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
     resolve_aliases(e);
     if (e->reg_hand) {
         bool hand = false;
-        for (const auto& pl : e->plans) hand |= pl.hand && pl.multi_blk;
+        for (const auto& pl : e->plans) hand |= (pl.hand && pl.multi_blk) || pl.npass > 1;
         if (!hand) {  // the autotuner picked classic blocks: free the device's entry
             std::lock_guard<std::mutex> lock(g_wait_mu);
             WaitReg& r = g_wait_reg[e->device];
@@ -1636,15 +1685,22 @@ gol_status step_resident(gol_engine* e, uint64_t generations)
     return GOL_OK;
 }
 
+// `passes` > 1: a multi-pass launch of that many depth-K passes (plans with npass
+// >= passes), reading buf[cur] and writing buf[cur + 1 .. cur + passes]
 gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
-                  hipStream_t stream = nullptr)
+                  hipStream_t stream = nullptr, int passes = 1)
 {
     hipStream_t s = stream ? stream : e->stream;
     const int region = (e->band_stream && s == e->band_stream) ? 1 : 0;
     const auto& p = e->plans[plan];
+    if (passes < 1 || (passes > 1 && (passes > p.npass || depth != e->K || !e->mpflags)))
+        return fail(GOL_ESTATE, "multi-pass launch of a plan without passes");
     StepArgs a{};
-    a.in = e->buf[e->cur];
-    a.out = e->buf[e->cur ^ 1];
+    for (int i = 0; i <= passes; ++i) a.pbuf[i] = e->buf[(e->cur + i) % e->nbuf];
+    a.npass = passes;
+    a.shadow_off = e->shadow_off;
+    a.mpflags = e->mpflags;
+    a.err = e->d_err;
     a.segs = p.dev;
     a.nseg = (int32_t)p.segs.size() + (p.pair_units ? 1 : 0);
     if (p.segs.size() == 1) {
@@ -1667,7 +1723,6 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     if (hand) {
         a.side = e->side[region];
         a.flags = e->flags[region];
-        a.err = e->d_err;
         a.side_slot = (int64_t)2 * (depth - 1) * 64 * (e->planes / 2);
         a.tail_off = gol::handoff_toff(p.rpw, (int)depth, e->planes);
         // The pair forms (life_stencil.h stage_rm) take a step's pair parity from
@@ -1713,10 +1768,10 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         const double cols = 64.0 * 32.0 * e->planes;  // per strip or unit
         double rows = 0;
         for (const auto& sg : p.segs) rows += (double)std::max<int64_t>(0, sg.out_hi - sg.out_lo);
-        GOL_TRY(timing_end(e, s, e0, e1, p.own_rows * (double)e->W * depth,
-                           (comp * p.groups + comp_half) * cols, rows));
+        GOL_TRY(timing_end(e, s, e0, e1, p.own_rows * (double)e->W * depth * passes,
+                           (comp * p.groups + comp_half) * cols * passes, rows * passes));
     }
-    if (swap) e->cur ^= 1;
+    if (swap) e->cur = (e->cur + passes) % e->nbuf;
     return GOL_OK;
 }
 
@@ -1805,7 +1860,7 @@ gol_status autotune_plans(gol_engine* e)
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
     if (st == GOL_OK) st = check_err(e);  // a hand-off wait that timed out is a failure here too
-    for (int b = 0; b < 2 && st == GOL_OK; ++b)
+    for (int b = 0; b < e->nbuf && st == GOL_OK; ++b)
         if (hipMemsetAsync(e->alloc[b], 0, words_all * sizeof(uint64_t), e->stream) != hipSuccess)
             st = fail(GOL_EHIP, "autotune: clearing the field");
     return st;
@@ -2363,11 +2418,13 @@ void gol_destroy(gol_engine* e)
     for (auto& p : e->plans) free_plan(p);
     for (auto& alts : e->plan_alts)
         for (auto& p : alts) free_plan(p);
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < 4; ++b)
         if (e->alloc[b]) (void)hipFree(e->alloc[b]);
+    for (int b = 0; b < 2; ++b) {
         if (e->side[b]) (void)hipFree(e->side[b]);
         if (e->flags[b]) (void)hipFree(e->flags[b]);
     }
+    if (e->mpflags) (void)hipFree(e->mpflags);
     if (e->d_err) (void)hipFree(e->d_err);
     if (e->res.flags) (void)hipFree(e->res.flags);
     for (hipEvent_t ev : {e->res.ev_in, e->res.ev_out})
@@ -2658,7 +2715,7 @@ gol_status run_launch_op(gol_engine* e, const SchedOp& op, Xchg&& xchg)
         return GOL_OK;
     case GOL_OP_INTERIOR:
         GOL_TRY(launch(e, op.plan, op.depth, false));  // interior, overlaps the exchange
-        e->cur ^= 1;
+        e->cur = (e->cur + 1) % e->nbuf;
         return GOL_OK;
     case GOL_OP_EXCHANGE_ASYNC:
         GOL_TRY(xchg());
@@ -2666,6 +2723,15 @@ gol_status run_launch_op(gol_engine* e, const SchedOp& op, Xchg&& xchg)
         return GOL_OK;
     default: return fail(GOL_ESTATE, "bad schedule op");
     }
+}
+
+// Passes of the next launch of plan `plan` at depth d with `left` generations to
+// go: multi-pass plans run up to npass full-depth passes per launch.
+int passes_for(const gol_engine* e, int plan, uint32_t d, uint64_t left)
+{
+    const int np = e->plans[(size_t)plan].npass;
+    if (np <= 1 || d != e->K) return 1;
+    return (int)std::min<uint64_t>((uint64_t)np, left / d);
 }
 
 // Single-stream engines: the launch sequence of gol_step(gens) as a captured
@@ -2694,8 +2760,9 @@ gol_status step_single(gol_engine* e, uint64_t generations)
             gol_status st = GOL_OK;
             while (left > 0 && st == GOL_OK) {
                 const uint32_t d = pick_depth(e->K, left);
-                st = launch(e, 0, d);
-                left -= d;
+                const int np = passes_for(e, 0, d, left);
+                st = launch(e, 0, d, true, nullptr, np);
+                left -= (uint64_t)d * np;
             }
             const hipError_t ce = hipStreamEndCapture(e->stream, &g);
             if (st != GOL_OK) {
@@ -2724,8 +2791,9 @@ gol_status step_single(gol_engine* e, uint64_t generations)
     }
     while (left > 0) {
         const uint32_t d = pick_depth(e->K, left);
-        GOL_TRY(launch(e, 0, d));
-        left -= d;
+        const int np = passes_for(e, 0, d, left);
+        GOL_TRY(launch(e, 0, d, true, nullptr, np));
+        left -= (uint64_t)d * np;
     }
     return GOL_OK;
 }
@@ -2749,7 +2817,21 @@ gol_status gol_step(gol_engine* e, uint64_t generations)
     };
     std::vector<SchedOp> ops;
     step_schedule(e->K, e->Hx, e->overlap, e->halo_fresh, generations, ops);
-    for (const SchedOp& op : ops) {
+    // consecutive full-depth launch ops of one block plan (the shared region of a
+    // round, rank_geometry) run as one multi-pass launch when the plan has passes
+    auto root = [e](int pi) { return e->plan_alias[(size_t)pi] >= 0 ? e->plan_alias[(size_t)pi] : pi; };
+    for (size_t i = 0; i < ops.size(); ++i) {
+        const SchedOp& op = ops[i];
+        if (op.kind == GOL_OP_LAUNCH && op.depth == e->K && e->plans[(size_t)op.plan].npass > 1) {
+            int n = 1;
+            while (n < e->plans[(size_t)op.plan].npass && i + n < ops.size() &&
+                   ops[i + n].kind == GOL_OP_LAUNCH && ops[i + n].depth == e->K &&
+                   root(ops[i + n].plan) == root(op.plan))
+                ++n;
+            GOL_TRY(launch(e, op.plan, op.depth, true, nullptr, n));
+            i += (size_t)n - 1;
+            continue;
+        }
         if (op.kind == GOL_OP_EXCHANGE) {
             GOL_TRY(exchange(e, e->stream));
         } else if (op.kind == GOL_OP_WAIT_EXCHANGE) {
@@ -2959,6 +3041,17 @@ gol_status gol_plan_tuning(gol_engine* e, uint32_t* variant, float* tuned_us, fl
     if (variant) *variant = on ? (uint32_t)p.tuned : 0u;
     if (tuned_us) *tuned_us = on ? 1e3f * p.tune_ms : 0.f;
     if (model_us) *model_us = on ? 1e3f * p.tune_ms_model : 0.f;
+    return GOL_OK;
+}
+
+gol_status gol_plan_passes(gol_engine* e, uint32_t* passes)
+{
+    if (!e || !passes) return fail(GOL_EINVAL, "null argument");
+    if (!e->parts.empty()) return gol_plan_passes(e->parts[0], passes);
+    if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
+    const bool rk = e->nranks > 1 && e->Hx >= e->K;
+    const auto& p = rk ? e->plans[e->K - 1] : e->plans[0];
+    *passes = e->res.on ? 1u : (uint32_t)p.npass;
     return GOL_OK;
 }
 

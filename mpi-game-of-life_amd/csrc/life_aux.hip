@@ -12,7 +12,7 @@ namespace gol {
 #define GOL_EXTERN_DEPTH(K)                                                                   \
     extern template hipError_t launch_depth<K>(const StepArgs&, RuleKind, int, bool,          \
                                                hipStream_t);                                  \
-    extern template int occupancy_depth<K>(RuleKind, int, bool);
+    extern template int occupancy_depth<K>(RuleKind, int, bool, bool);
 GOL_EXTERN_DEPTH(1)
 GOL_EXTERN_DEPTH(2)
 GOL_EXTERN_DEPTH(4)
@@ -50,21 +50,21 @@ hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int planes, 
     }
 }
 
-int life_blocks_per_cu(int depth, RuleKind rule, int planes, bool hand)
+int life_blocks_per_cu(int depth, RuleKind rule, int planes, bool hand, bool mp)
 {
     switch (depth) {
-    case 1: return occupancy_depth<1>(rule, planes, hand);
-    case 2: return occupancy_depth<2>(rule, planes, hand);
-    case 4: return occupancy_depth<4>(rule, planes, hand);
-    case 6: return occupancy_depth<6>(rule, planes, hand);
-    case 7: return occupancy_depth<7>(rule, planes, hand);
-    case 8: return occupancy_depth<8>(rule, planes, hand);
-    case 12: return occupancy_depth<12>(rule, planes, hand);
-    case 16: return occupancy_depth<16>(rule, planes, hand);
+    case 1: return occupancy_depth<1>(rule, planes, hand, mp);
+    case 2: return occupancy_depth<2>(rule, planes, hand, mp);
+    case 4: return occupancy_depth<4>(rule, planes, hand, mp);
+    case 6: return occupancy_depth<6>(rule, planes, hand, mp);
+    case 7: return occupancy_depth<7>(rule, planes, hand, mp);
+    case 8: return occupancy_depth<8>(rule, planes, hand, mp);
+    case 12: return occupancy_depth<12>(rule, planes, hand, mp);
+    case 16: return occupancy_depth<16>(rule, planes, hand, mp);
 #if GOL_DEV_KERNELS
-    case 20: return occupancy_depth<20>(rule, planes, hand);
-    case 24: return occupancy_depth<24>(rule, planes, hand);
-    case 32: return occupancy_depth<32>(rule, planes, hand);
+    case 20: return occupancy_depth<20>(rule, planes, hand, mp);
+    case 24: return occupancy_depth<24>(rule, planes, hand, mp);
+    case 32: return occupancy_depth<32>(rule, planes, hand, mp);
 #endif
     default: return 0;
     }

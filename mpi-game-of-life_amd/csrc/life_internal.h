@@ -49,8 +49,15 @@ constexpr int kGuardRows = 64;
 constexpr int kMaxDepth = 32;
 
 struct StepArgs {
-    const uint64_t* in;   // state buffer row 0 (guard rows precede it)
-    uint64_t* out;
+    // state buffers, row 0 (guard rows precede it): pass p of the launch reads
+    // pbuf[p] and writes pbuf[p + 1]
+    uint64_t* pbuf[4];
+    // multi-pass launches (life_stencil.h): passes (1 = single), the byte offset of
+    // the halo lanes' shadow half of each buffer, and the head/done flags (4 x
+    // total_units words, all 0 between launches)
+    int32_t npass;
+    uint32_t shadow_off;
+    uint32_t* mpflags;
     const SegDesc* segs;  // device table
     int32_t nseg;
     int32_t strips;       // strip groups per row: ceil(ceil(wq / (L-2)) / (64/L))
@@ -70,8 +77,8 @@ struct StepArgs {
     // Row-block hand-off (kernels instantiated with HAND = true; see
     // life_stencil.h): each wavefront's slot of side rows, its ready flag, and a
     // flag the kernel sets when a wait for a neighbour's rows timed out.
-    uint64_t* side;       // total_units slots of side_slot words
-    uint32_t* flags;      // total_units words, zeroed before every launch
+    uint64_t* side;       // total_units slots of side_slot words (per pass parity)
+    uint32_t* flags;      // total_units words (per pass parity), all 0 between launches
     int* err;
     int64_t side_slot;    // words per slot: 2 (K-1) rows x 64 lanes x NP/2 words
     uint64_t* wlog;       // dev timing builds only (GOL_EXP & 128): 8 words per wavefront
@@ -119,6 +126,14 @@ constexpr bool handoff_kernel_exists(int K, RuleKind rule)
     return K >= kHandoffMinDepth && (rule != RULE_GENERIC || K <= 12);
 }
 
+// Multi-pass stencil kernels (StepArgs::npass > 1, life_stencil.h): 2-plane lane
+// groups at depths 12 and 16 (the generic-mask rule at 12 only, as its hand-off
+// kernels)
+constexpr bool multipass_kernel_exists(int K, RuleKind rule, int planes)
+{
+    return planes == 2 && (K == 12 || (K == 16 && rule != RULE_GENERIC));
+}
+
 // Steps per block of the stencil kernel's register prefetch ring (host copy of
 // life_stencil.h kPfOf): 8 for 2-plane kernels of depth >= 16, 4 elsewhere.
 constexpr int prefetch_of(int K, int planes) { return (planes == 2 && K >= 16) ? 8 : 4; }
@@ -157,13 +172,14 @@ hipError_t launch_life(const StepArgs& a, int depth, RuleKind rule, int planes, 
 bool life_has_kernel(int depth, int planes);
 
 // Resident 256-thread blocks per CU of the stencil kernel (occupancy query).
-int life_blocks_per_cu(int depth, RuleKind rule, int planes, bool hand);
+// mp: of the multi-pass kernels (0 where none exists)
+int life_blocks_per_cu(int depth, RuleKind rule, int planes, bool hand, bool mp = false);
 
 // Per-depth entry points (explicitly instantiated in life_tb_d<K>.hip).
 template <int K>
 hipError_t launch_depth(const StepArgs& a, RuleKind rule, int planes, bool hand, hipStream_t s);
 template <int K>
-int occupancy_depth(RuleKind rule, int planes, bool hand);
+int occupancy_depth(RuleKind rule, int planes, bool hand, bool mp);
 
 // The resident kernel (life_resident.hip): one launch runs a whole gol_step on a
 // small field held in registers by one 1024-thread workgroup per (band, strip)

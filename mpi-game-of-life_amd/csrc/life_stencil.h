@@ -490,7 +490,9 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 #define GOL_WARM_PREFETCH 1
 #endif
 
-template <int K, int RULE, int NP, bool HAND, int TOFF>
+// MP: the multi-pass form (StepArgs::npass > 1; a separate instantiation, so the
+// single-pass kernel's steady loop stays exactly as it was)
+template <int K, int RULE, int NP, bool HAND, int TOFF, bool MP = false>
 // (capped at 256 registers to keep 2 waves per SIMD: the 8-step-prefetch hand-off
 // kernels of tail offset 2, which need 258 VGPRs, with a few scratch spills, and the
 // B/S2 and B3/S23 ones with the pair sum, whose hand-off kernels would take 262)
@@ -650,46 +652,143 @@ void life_tb_kernel(StepArgs a)
     // step counts and indices are 32-bit (a block has at most rows_per_wave + 2K
     // steps): uniform 32-bit compares stay on the scalar unit, 64-bit ones do not
     const int32_t T = (int32_t)(re - rb) + 2 * K;  // steps (input rows of a classic block)
-    const int64_t row_first = rb - K;              // local row of step 0
     // hand-off roles: every block but the top one produces side rows for the block
     // above; every block but the bottom one consumes those of the block below
     // (pair units close their blocks the classic way: their segment, the last of
     // the launch, is one block deep.  A pu term here instead costs the hand-off
     // kernels ~80 VGPRs: the compiler specializes the stream on it.)
-    const bool producer = HAND && blk > 0;
-    const bool consumer = HAND && blk < sg.nblk - 1;
-    // a consumer streams R + 2 input rows (steps < t_side), then side rows
-    const int32_t t_side = consumer ? (int32_t)(re - rb) + 2 : INT32_MAX;
-
-    const char* in_rows = reinterpret_cast<const char*>(a.in + (sg.base_row + row_first) * a.stride);
-    char* out_rows = reinterpret_cast<char*>(a.out + (sg.base_row + rb) * a.stride);
     const int64_t row_bytes = a.stride * 8;
     constexpr int64_t kSideRowBytes = 64 * G * 8;
-    char* my_side = HAND ? reinterpret_cast<char*>(a.side + unit * a.side_slot) : nullptr;
-    const char* dn_side =
-        HAND ? reinterpret_cast<const char*>(a.side + (unit - a.strips) * a.side_slot) : nullptr;
     const bool st_lane = qin && exact;
+    // buffer rows that are inside the buffer and the field (dead border)
+    const int64_t vlo = max((int64_t)0, -sg.glob0), vhi = min(sg.in_rows, sg.field_h - sg.glob0);
+    const bool has_above = blk > 0, has_below = blk < sg.nblk - 1;
 
-    // field-row validity of the row of step t (dead border) and buffer-row validity:
-    // steps [t_lo, t_hi) read rows inside both
-    const int32_t t_lo = (int32_t)(max((int64_t)0, -sg.glob0) - row_first);
-    const int32_t t_hi = (int32_t)(min(sg.in_rows, sg.field_h - sg.glob0) - row_first);
-    // field rows of stage outputs: stage g at step t emits field row
-    // glob0 + row_first + t - (g+1), alive only in [0, field_h)
-    const int32_t f_lo = (int32_t)(-(sg.glob0 + row_first));
-    const int32_t f_hi = (int32_t)(sg.field_h - (sg.glob0 + row_first));
+    // Multi-pass launches (r05).  A launch runs `npass` passes of K generations
+    // over the same row blocks, pass p reading buffer pbuf[p] and writing
+    // pbuf[p + 1] (the host gives npass + 1 distinct buffers, so no pass writes
+    // rows another wavefront may still read in an earlier pass).  Odd passes
+    // stream their block bottom-up: a block's first rows in one pass are then its
+    // last ones in the next, so the rows beyond its start (the block in front,
+    // "front") were computed at that block's start of the previous pass, long
+    // done, and only the rows beyond its end (the block behind, "back") wait for
+    // a neighbour to finish the previous pass -- at the end of this one.  Flags:
+    // a unit raises head[p] once its first K output rows of pass p are stored and
+    // done[p] at the end of pass p, each read (and reset) by the one unit that
+    // needs it.  Halo lanes (lanes whose group another strip outputs) keep their
+    // own values across passes in a shadow half of each buffer (a.shadow_off
+    // bytes on): after P passes of K generations their outer P*K columns are wrong
+    // and the exact lanes beside them still see exact columns (P*K <= 48 < 64).
+    // The stencil is symmetric under a vertical flip, so a bottom-up pass is the
+    // same code on rows addressed with a negative stride.
+    const int npass = MP ? a.npass : 1;
+    const bool halo_lane = qin && !exact && !pu;
+    bool up = false, producer = false, consumer = false, head_sent = false;
+    int32_t t_side = INT32_MAX, t_lo = 0, t_hi = 0, f_lo = 0, f_hi = 0;
+    int32_t s_back = INT32_MAX;  // first stream step beyond the block's far end
+    int64_t rs = row_bytes;      // bytes per stream step (negative bottom-up)
+    const char* in_rows = nullptr;
+    char* out_rows = nullptr;
+    char* my_side = nullptr;
+    const char* dn_side = nullptr;
+    uint32_t* my_flag = nullptr;
+    uint32_t* dn_flag = nullptr;
+    uint32_t voff_ld = voff, voff_st = voff;
+    bool st_ok = st_lane, wt_stores = false, done_need = false, back_need = false;
+    int64_t back_unit = 0;
+    // one-shot flags of the multi-pass protocol: wait until *f is set, reset it
+    auto mp_wait = [&](uint32_t* f) {
+        uint32_t v = 0;
+        uint64_t w0 = 0;
+        for (int it = 0;; ++it) {
+            v = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (v) break;
+            if (it == 0) w0 = wait_clock();
+            else if (wait_clock() - w0 > kWaitTicks) break;
+            __builtin_amdgcn_s_sleep(4);
+        }
+        if (lane == 0) {
+            if (!v) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("" ::: "memory");
+    };
+    auto mp_raise = [&](uint32_t* f) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pass's stores drained
+        if (lane == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // flags of unit x for pass p: head at [p][x], done at [2 + p][x]
+    auto head_flag = [&](int p, int64_t x) { return a.mpflags + (int64_t)p * a.total_units + x; };
+    auto done_flag = [&](int p, int64_t x) { return a.mpflags + (int64_t)(2 + p) * a.total_units + x; };
 
+#if GOL_EXP & 128
+    uint64_t wl_tb = 0, wl_tb1 = 0, wl_tw = 0, wl_ts = 0;
+#endif
+#if GOL_EXP & 16384
+    uint64_t wl_pi = 0, wl_pl = 0;
+#endif
+    for (int pass = 0; pass < npass; ++pass) {
+    {
+        up = (pass & 1) != 0;
+        const int64_t start_row = up ? re - 1 + K : rb - K;  // local row of step 0
+        const int64_t out_first = up ? re - 1 : rb;          // row of the first output
+        rs = up ? -row_bytes : row_bytes;
+        in_rows = reinterpret_cast<const char*>(a.pbuf[pass] + (sg.base_row + start_row) * a.stride);
+        out_rows = reinterpret_cast<char*>(a.pbuf[pass + 1] + (sg.base_row + out_first) * a.stride);
+        // steps [t_lo, t_hi) read rows inside the buffer and the field
+        t_lo = (int32_t)(up ? start_row - vhi + 1 : vlo - start_row);
+        t_hi = (int32_t)(up ? start_row - vlo + 1 : vhi - start_row);
+        // stage g at step t emits the row t - (g + 1) steps from start_row: a field
+        // row (glob0 + that row) alive only in [0, field_h) when x in [f_lo, f_hi)
+        f_lo = (int32_t)(up ? sg.glob0 + start_row - sg.field_h + 1 : -(sg.glob0 + start_row));
+        f_hi = (int32_t)(up ? sg.glob0 + start_row + 1 : sg.field_h - (sg.glob0 + start_row));
+        // hand-off roles: a block takes its last side rows from the block behind it
+        // (top-down: the block below, bottom-up: the block above) and produces them
+        // for the block in front (pair units close their blocks the classic way:
+        // their segment, the last of the launch, is one block deep)
+        producer = HAND && (up ? has_below : has_above);
+        consumer = HAND && (up ? has_above : has_below);
+        // a consumer streams R + 2 input rows (steps < t_side), then side rows
+        t_side = consumer ? (int32_t)(re - rb) + 2 : INT32_MAX;
+        s_back = (int32_t)(re - rb) + (consumer ? 0 : K);
+        const int64_t par = pass & 1;
+        const int64_t prod = up ? unit + a.strips : unit - a.strips;  // a consumer's producer
+        if constexpr (HAND) {
+            my_side = reinterpret_cast<char*>(a.side + (par * a.total_units + unit) * a.side_slot);
+            dn_side = reinterpret_cast<const char*>(a.side + (par * a.total_units + prod) * a.side_slot);
+            my_flag = a.flags + par * a.total_units + unit;
+            dn_flag = a.flags + par * a.total_units + prod;
+        }
+        voff_ld = voff + ((pass > 0 && halo_lane) ? a.shadow_off : 0u);
+        const bool wr_shadow = pass < npass - 1 && halo_lane;
+        voff_st = voff + (wr_shadow ? a.shadow_off : 0u);
+        st_ok = st_lane || wr_shadow;
+        // rows another wavefront reads in the next pass go out write-through
+        wt_stores = pass < npass - 1;
+        // the next pass's reader of this pass's head / done flags (see above)
+        head_sent = !(pass < npass - 1 && (up ? has_below : has_above));
+        done_need = pass < npass - 1 && (up ? has_above : has_below);
+        back_need = pass > 0 && (up ? has_above : has_below);
+        back_unit = up ? unit + a.strips : unit - a.strips;
+        // the block in front's first rows of the previous pass
+        if (pass > 0 && (up ? has_below : has_above))
+            mp_wait(head_flag(pass - 1, up ? unit - a.strips : unit + a.strips));
+        // the block behind's last rows of the previous pass, when the rows the pass
+        // loads up front reach them (later: mp_sync)
+        if (back_need && s_back < kWarmSteps + 2 * kPrefetch) mp_wait(done_flag(pass - 1, back_unit));
+    }
     StageT<NP> st[K];
 #pragma unroll
     for (int g = 0; g < K; ++g) st[g] = {};
 
-    // the row streamed at step s: input row row_first + s, or for a consumer from
+    // the row streamed at step s: input row start_row + s (rows in stream order), or for a consumer from
     // step t_side on the block below's side row s - t_side (uniform select)
     auto load_step = [&](int32_t s) -> Grp<NP> {
         if constexpr (!HAND)
-            return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
+            return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * rs + voff_ld));
         if (s < t_side)
-            return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
+            return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * rs + voff_ld));
         // side rows: stored sc1 by another wavefront of this launch, loaded sc1
         return load_grp<NP>(reinterpret_cast<const uint64_t*>(
             dn_side + (int64_t)(s - t_side) * kSideRowBytes + voff_side));
@@ -706,7 +805,7 @@ void life_tb_kernel(StepArgs a)
     Grp<NP> wring[kWarmSteps];
 #pragma unroll
     for (int p = 0; p < kWarmSteps; ++p)  // (input rows: t_side >= warm-up + 2 blocks)
-        wring[p] = load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)p * row_bytes + voff));
+        wring[p] = load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)p * rs + voff_ld));
     constexpr int kSteadyIssue = kWarmSteps >= 2 * kPrefetch ? kWarmSteps - 2 * kPrefetch : 0;
 #else
 #pragma unroll
@@ -715,9 +814,9 @@ void life_tb_kernel(StepArgs a)
 #if GOL_EXP & 16384
     // dev probe of a wavefront's start (tools/wave_log.py --probe): the initial
     // loads issued, and all of them landed (results stay valid, timing does not)
-    const uint64_t wl_pi = __builtin_amdgcn_s_memrealtime();
+    wl_pi = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint64_t wl_pl = __builtin_amdgcn_s_memrealtime();
+    wl_pl = __builtin_amdgcn_s_memrealtime();
 #endif
 
     // row of step t: an input row is dead outside the field / buffer; a side row
@@ -731,14 +830,14 @@ void life_tb_kernel(StepArgs a)
         return x;
     };
     auto load_in = [&](int32_t s) -> Grp<NP> {
-        return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * row_bytes + voff));
+        return load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)s * rs + voff_ld));
     };
-    // stage g (generation g+1) at step t: emits local row row_first + t - (g+1)
+    // stage g (generation g+1) at step t: emits the row t - (g+1) steps from start_row
     // With births (rules other than B/S2) nothing may come alive outside the field:
     // rm is the uniform row test of the emitted row (all ones or 0, a scalar), the
     // column mask is per lane; one v_bitop3 AND3 per plane (8-byte encoding, like the
     // rest of the hot loop).
-    auto row_mask = [&](int32_t r) -> uint32_t {  // r: field row relative to glob0 + row_first
+    auto row_mask = [&](int32_t r) -> uint32_t {  // r: steps from start_row of the emitted row
         return __builtin_amdgcn_readfirstlane((r >= f_lo) && (r < f_hi) ? ~0u : 0u);
     };
     // (the ingested row of stage g at step t is t - g; every caller's t has the parity
@@ -778,18 +877,46 @@ void life_tb_kernel(StepArgs a)
         t_plain_end = INT32_MIN;  // dev A/B: every steady block masked (r03 behaviour)
 #endif
     }
-    auto store = [&](int32_t t, const Pl<NP>& x) {
-        if (t >= 2 * K && t < T && st_lane) {
+    // (wt: wt_stores as the caller's opaque copy, see `opaque`)
+    auto store = [&](int32_t t, const Pl<NP>& x, uint32_t wt) {
+        if (t >= 2 * K && t < T && st_ok) {
+            char* o = out_rows + (int64_t)(t - 2 * K) * rs + voff_st;
+            if (wt) {
+                store_side<NP>(reinterpret_cast<uint64_t*>(o), x);
+            } else {
 #if GOL_NT_STORES
-            const Grp<NP> g = words_of(x);
-            uint64_t* o = reinterpret_cast<uint64_t*>(out_rows + (int64_t)(t - 2 * K) * row_bytes + voff);
+                const Grp<NP> g = words_of(x);
 #pragma unroll
-            for (int i = 0; i < NP / 2; ++i) __builtin_nontemporal_store(g.w[i], o + i);
+                for (int i = 0; i < NP / 2; ++i)
+                    __builtin_nontemporal_store(g.w[i], reinterpret_cast<uint64_t*>(o) + i);
 #else
-            *reinterpret_cast<Grp<NP>*>(out_rows + (int64_t)(t - 2 * K) * row_bytes + voff) =
-                words_of(x);
+                *reinterpret_cast<Grp<NP>*>(o) = words_of(x);
 #endif
+            }
         }
+    };
+    // A uniform value the compiler must treat as new in every block: tests of the
+    // per-pass state (write-through stores, the multi-pass flags) would otherwise
+    // be hoisted out of the steady loop, which then exists twice (unswitched) and
+    // loses its code placement (tools/loop_align.py).
+    auto opaque = [](uint32_t v) {
+        v = __builtin_amdgcn_readfirstlane(v);
+        asm volatile("" : "+s"(v));
+        return v;
+    };
+    // (multi-pass) after the stores of the steps up to t_last: the head flag once
+    // the block's first K output rows (steps 2K .. 3K-1) are out
+    auto head_check = [&](int32_t t_last) {
+        if (!head_sent && t_last >= 3 * K - 1) {
+            mp_raise(head_flag(pass, unit));
+            head_sent = true;
+        }
+    };
+    // (multi-pass) in the steady block from t0, before the refill of the block after
+    // it: the block behind's done flag when that refill reaches step s_back
+    auto mp_sync = [&](int32_t t0) {
+        if (back_need && s_back >= t0 + 2 * kPrefetch && s_back < t0 + 3 * kPrefetch)
+            mp_wait(done_flag(pass - 1, back_unit));
     };
 
     // Hand-off signalling (HAND kernels), done in steady blocks after the compute:
@@ -801,11 +928,10 @@ void life_tb_kernel(StepArgs a)
     //    R + 2 >= warm-up + 2 blocks + tail offset, handoff_toff).
     auto signal = [&]() {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_store(a.flags + unit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(my_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto wait_below = [&]() {
-        const uint32_t* f = a.flags + (unit - a.strips);
+        const uint32_t* f = dn_flag;
         uint32_t v = 0;
         uint64_t t0 = 0;
         for (int it = 0; !(GOL_EXP & 1); ++it) {
@@ -820,15 +946,18 @@ void life_tb_kernel(StepArgs a)
         if (lane == 0) {
             if (!v && !(GOL_EXP & 1))
                 __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // flags are all 0 between launches: reset the producer's
+            // flags are all 0 between launches (and passes of one parity): reset
+            // the producer's
             __hip_atomic_store(const_cast<uint32_t*>(f), 0u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("" ::: "memory");
     };
     auto sync_point = [&](int32_t t0) {
-        if (producer && t0 == kWarmSteps && !(GOL_EXP & 2)) signal();
-        if (consumer && t0 + 3 * kPrefetch + TOFF > t_side && t0 + 2 * kPrefetch + TOFF <= t_side)
+        const uint32_t r0 = (producer ? 1u : 0u) | (consumer ? 2u : 0u);
+        const uint32_t role = MP ? opaque(r0) : r0;
+        if ((role & 1u) && t0 == kWarmSteps && !(GOL_EXP & 2)) signal();
+        if ((role & 2u) && t0 + 3 * kPrefetch + TOFF > t_side && t0 + 2 * kPrefetch + TOFF <= t_side)
             wait_below();
     };
 
@@ -887,7 +1016,8 @@ void life_tb_kernel(StepArgs a)
         }
         if constexpr (!kGuard) {
             __builtin_amdgcn_sched_barrier(0);
-            place_block<life_loop_pad(K, RULE, NP, HAND, TOFF, kMask ? 1 : 0) != 0, NP, kPrefetch>(x);
+            place_block<life_loop_pad(K, RULE, NP, HAND, TOFF, (kMask ? 1 : 0) | (MP ? 2 : 0)) != 0, NP,
+                        kPrefetch>(x);
             __builtin_amdgcn_sched_barrier(0);
         }
         // stage g of step p only needs stage g-1 of step p and stage g of step
@@ -941,15 +1071,18 @@ void life_tb_kernel(StepArgs a)
             // previous block's stores) were issued a whole block of compute ago
             if constexpr (HAND) sync_point(t0);
         }
+        const uint32_t wt = MP ? opaque(wt_stores ? 1u : 0u) : 0u;
+        if constexpr (MP && !kGuard) mp_sync(t0);
 #pragma unroll
-        for (int p = 0; p < kPrefetch; ++p) store(t0 + p, x[p]);
+        for (int p = 0; p < kPrefetch; ++p) store(t0 + p, x[p], wt);
+        if constexpr (MP) head_check(t0 + kPrefetch - 1);
     };
 
     // Warm-up blocks, unrolled (compile-time guards).
     constexpr int kWarm = kWarmSteps;
     static_assert(!HAND || kWarm >= 2 * K, "side rows are all stored in the warm-up blocks");
 #if GOL_EXP & 128
-    uint64_t wl_tb = 0, wl_tb1 = 0;  // after the first / second warm-up block
+    // (wl_tb / wl_tb1: after the first / second warm-up block)
 #pragma unroll
     for (int t0 = 0; t0 < kWarm; t0 += kPrefetch) {
         block(t0, std::integral_constant<int, kWarmBlk>{});
@@ -962,7 +1095,7 @@ void life_tb_kernel(StepArgs a)
 #endif
 #if GOL_EXP & 128
     // phase stamps (r05): issue time of the warm-up's end and the steady blocks' end
-    const uint64_t wl_tw = __builtin_amdgcn_s_memrealtime();
+    wl_tw = __builtin_amdgcn_s_memrealtime();
 #endif
 
     // Steady state: whole blocks of input steps.  A consumer stops TOFF steps
@@ -979,9 +1112,8 @@ void life_tb_kernel(StepArgs a)
 #endif
     } else {
         // the consumer's wait is in the last pure block
-        auto pure_more = [&](int32_t t) {
-            return consumer ? t + 2 * kPrefetch + TOFF <= t_side : t < T;
-        };
+        const int32_t t_pure_end = consumer ? t_side - 2 * kPrefetch - TOFF + 1 : T;
+        auto pure_more = [&](int32_t t) { return t < t_pure_end; };
         for (; pure_more(t0) && t0 < t_plain_end; t0 += kPrefetch)
             block(t0, std::integral_constant<int, kPure>{});
         if constexpr (kBirths)
@@ -995,7 +1127,7 @@ void life_tb_kernel(StepArgs a)
     if constexpr (HAND)
         if (producer && T <= kWarm && !(GOL_EXP & 2)) signal();
 #if GOL_EXP & 128
-    const uint64_t wl_ts = __builtin_amdgcn_s_memrealtime();
+    wl_ts = __builtin_amdgcn_s_memrealtime();
 #endif
 
     if constexpr (HAND && !(GOL_EXP & 8)) {
@@ -1020,8 +1152,10 @@ void life_tb_kernel(StepArgs a)
                         if (g >= 0 && g < K) x[p] = stage(g, p, t0 + p, x[p]);
                     }
                 }
+                const uint32_t wt = MP ? opaque(wt_stores ? 1u : 0u) : 0u;
 #pragma unroll
-                for (int p = 0; p < TOFF; ++p) store(t0 + p, x[p]);
+                for (int p = 0; p < TOFF; ++p) store(t0 + p, x[p], wt);
+                if constexpr (MP) head_check(t0 + TOFF - 1);
             }
             // Tail: steps t_side + tau, tau = 0 .. 2K-3.  Side row tau (generation
             // tau/2 + 1) enters at stage s0 = tau/2 + 1 in place of stage s0-1's
@@ -1044,14 +1178,24 @@ void life_tb_kernel(StepArgs a)
                             x[p] = stage(g, p, tb + tau, x[p]);
                     }
                 }
+                const uint32_t wt = MP ? opaque(wt_stores ? 1u : 0u) : 0u;
 #pragma unroll
                 for (int p = 0; p < kPrefetch; ++p)
-                    if (tau0 + p < kSideRows) store(tb + tau0 + p, x[p]);
+                    if (tau0 + p < kSideRows) store(tb + tau0 + p, x[p], wt);
+                if constexpr (MP) head_check(tb + tau0 + kPrefetch - 1);
             };
 #pragma unroll
             for (int tau0 = 0; tau0 < kSideRows; tau0 += kPrefetch) tail(tau0);
         }
     }
+    if (pass < npass - 1) {
+        // this pass's rows are out (this wavefront reads them next pass) and, for
+        // the wavefronts beside it, flagged
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!head_sent) mp_raise(head_flag(pass, unit));
+        if (done_need) mp_raise(done_flag(pass, unit));
+    }
+    }  // pass
 #if GOL_EXP & 128
     if (a.wlog && lane == 0) {
         // 8 words per wavefront: start, end, HW_ID | XCC_ID, block | workgroup,
@@ -1082,6 +1226,26 @@ hipError_t launch_kernel(const StepArgs& a, RuleKind rule, hipStream_t s)
 {
     const dim3 grid((unsigned)((a.total_units + kWavesPerBlock - 1) / kWavesPerBlock));
     const dim3 block(64 * kWavesPerBlock);
+    if (a.npass > 1) {
+        if constexpr (multipass_kernel_exists(K, RULE_REF, NP)) {
+            switch (rule) {
+            case RULE_REF:
+                hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, NP, HAND, TOFF, true>), grid, block, 0, s, a);
+                break;
+            case RULE_CONWAY:
+                hipLaunchKernelGGL((life_tb_kernel<K, RULE_CONWAY, NP, HAND, TOFF, true>), grid, block, 0, s, a);
+                break;
+            default:
+                if constexpr (multipass_kernel_exists(K, RULE_GENERIC, NP))
+                    hipLaunchKernelGGL((life_tb_kernel<K, RULE_GENERIC, NP, HAND, TOFF, true>), grid, block, 0, s, a);
+                else
+                    return hipErrorInvalidValue;
+                break;
+            }
+            return hipGetLastError();
+        }
+        return hipErrorInvalidValue;
+    }
     switch (rule) {
     case RULE_REF:
         hipLaunchKernelGGL((life_tb_kernel<K, RULE_REF, NP, HAND, TOFF>), grid, block, 0, s, a);
@@ -1100,11 +1264,25 @@ hipError_t launch_kernel(const StepArgs& a, RuleKind rule, hipStream_t s)
 }
 
 template <int K, int NP, bool HAND, int TOFF>
-int occupancy_kernel(RuleKind rule)
+int occupancy_kernel(RuleKind rule, bool mp)
 {
     int blocks = 0;
     hipError_t e = hipErrorInvalidValue;
     const int threads = 64 * kWavesPerBlock;
+    if (mp) {
+        if constexpr (multipass_kernel_exists(K, RULE_REF, NP)) {
+            if (rule == RULE_REF)
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &blocks, life_tb_kernel<K, RULE_REF, NP, HAND, TOFF, true>, threads, 0);
+            else if (rule == RULE_CONWAY)
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &blocks, life_tb_kernel<K, RULE_CONWAY, NP, HAND, TOFF, true>, threads, 0);
+            else if constexpr (multipass_kernel_exists(K, RULE_GENERIC, NP))
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &blocks, life_tb_kernel<K, RULE_GENERIC, NP, HAND, TOFF, true>, threads, 0);
+        }
+        return e == hipSuccess ? blocks : 0;
+    }
     if (rule == RULE_REF)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &blocks, life_tb_kernel<K, RULE_REF, NP, HAND, TOFF>, threads, 0);
@@ -1158,33 +1336,33 @@ hipError_t launch_depth(const StepArgs& a, RuleKind rule, int planes, bool hand,
 // 258 VGPRs and is capped), since a hand-off launch must fit in one round of
 // whichever offset its row lengths select (pick_rows_per_wave).
 template <int K, int NP>
-int occupancy_hand(RuleKind rule)
+int occupancy_hand(RuleKind rule, bool mp)
 {
     constexpr int pf = kPfOf<NP, K>();
-    int occ = occupancy_kernel<K, NP, true, 0>(rule);
-    occ = std::min(occ, occupancy_kernel<K, NP, true, pf / 2>(rule));
+    int occ = occupancy_kernel<K, NP, true, 0>(rule, mp);
+    occ = std::min(occ, occupancy_kernel<K, NP, true, pf / 2>(rule, mp));
     if constexpr (pf == 8) {
-        occ = std::min(occ, occupancy_kernel<K, NP, true, (pf == 8 ? 2 : 0)>(rule));
-        occ = std::min(occ, occupancy_kernel<K, NP, true, (pf == 8 ? 6 : 0)>(rule));
+        occ = std::min(occ, occupancy_kernel<K, NP, true, (pf == 8 ? 2 : 0)>(rule, mp));
+        occ = std::min(occ, occupancy_kernel<K, NP, true, (pf == 8 ? 6 : 0)>(rule, mp));
     }
     return occ;
 }
 
 template <int K>
-int occupancy_depth(RuleKind rule, int planes, bool hand)
+int occupancy_depth(RuleKind rule, int planes, bool hand, bool mp)
 {
     if (hand && K < kHandoffMinDepth) return 0;
     if (planes == 4) {
         if constexpr (depth_has_planes(K, 4)) {
             if constexpr (K >= kHandoffMinDepth)
-                if (hand) return occupancy_hand<K, 4>(rule);
-            return occupancy_kernel<K, 4, false, 0>(rule);
+                if (hand) return occupancy_hand<K, 4>(rule, mp);
+            return occupancy_kernel<K, 4, false, 0>(rule, mp);
         }
         return 0;
     }
     if constexpr (K >= kHandoffMinDepth)
-        if (hand) return occupancy_hand<K, 2>(rule);
-    return occupancy_kernel<K, 2, false, 0>(rule);
+        if (hand) return occupancy_hand<K, 2>(rule, mp);
+    return occupancy_kernel<K, 2, false, 0>(rule, mp);
 }
 
 // Instantiation per depth.  A depth's hand-off kernels can be split into their
@@ -1192,13 +1370,13 @@ int occupancy_depth(RuleKind rule, int planes, bool hand)
 // in the others) to keep the build parallel.
 #define GOL_INSTANTIATE_DEPTH(K)                                                              \
     template hipError_t launch_depth<K>(const StepArgs&, RuleKind, int, bool, hipStream_t);   \
-    template int occupancy_depth<K>(RuleKind, int, bool);
+    template int occupancy_depth<K>(RuleKind, int, bool, bool);
 #define GOL_INSTANTIATE_HAND(K, T)                                                            \
     template hipError_t launch_kernel<K, 2, true, T>(const StepArgs&, RuleKind, hipStream_t); \
-    template int occupancy_kernel<K, 2, true, T>(RuleKind);
+    template int occupancy_kernel<K, 2, true, T>(RuleKind, bool);
 #define GOL_EXTERN_HAND(K, T)                                                                 \
     extern template hipError_t launch_kernel<K, 2, true, T>(const StepArgs&, RuleKind,        \
                                                             hipStream_t);                     \
-    extern template int occupancy_kernel<K, 2, true, T>(RuleKind);
+    extern template int occupancy_kernel<K, 2, true, T>(RuleKind, bool);
 
 }  // namespace gol

@@ -27,8 +27,9 @@ import tempfile
 LLVM = "/opt/rocm/lib/llvm/bin"
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = os.path.join(HERE, "..", "mpi-game-of-life_amd", "csrc", "loop_place.h")
-KRE = re.compile(r"^[0-9a-f]+ <_ZN3gol12_GLOBAL__N_114life_tb_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)EEEvNS_8StepArgsE>:")
-NRE = re.compile(r"life_tb_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)EEEvNS_8StepArgsE")
+# life_tb_kernel<K, RULE, NP, HAND, TOFF, MP> (MP, r05: the multi-pass form)
+KRE = re.compile(r"^[0-9a-f]+ <_ZN3gol12_GLOBAL__N_114life_tb_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)ELb(\d)EEEvNS_8StepArgsE>:")
+NRE = re.compile(r"life_tb_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)ELb(\d)EEEvNS_8StepArgsE")
 
 
 def disassemble_one(obj):
@@ -111,7 +112,9 @@ def main_loop_fractions(body, births):
     big = [c for c in inner if len(c[2]) >= 0.8 * top]
     frac = lambda e8: sum(1 for a in e8 if a % 8 == 4) / len(e8)
     if not births:
-        lo, hi, e8 = max(big, key=lambda c: len(c[2]))
+        # the pure loop: the smallest (r05: a hand-off consumer's last blocks, with
+        # the per-load side-row selects and the multi-pass checks, form bigger loops)
+        lo, hi, e8 = min(big, key=lambda c: len(c[2]))
         return [(0, frac(e8), len(e8))]
     small = min(len(c[2]) for c in big)
     out = []
@@ -139,8 +142,9 @@ def write_header(pads):
     open(HEADER, "w").write(f"""// loop_place.h -- GENERATED by tools/loop_align.py --update from the built
 // libgol.so; do not edit by hand.  life_loop_pad(K, RULE, NP, HAND, TOFF, MASK) = 1
 // adds a 4-byte s_nop after the 8-byte alignment before the compute of each
-// steady-state block of life_tb_kernel<K, RULE, NP, HAND, TOFF> without (MASK 0)
-// or with (MASK 1) the births mask (see life_stencil.h).
+// steady-state block of life_tb_kernel<K, RULE, NP, HAND, TOFF, MP> without (MASK
+// bit 0 clear) or with (bit 0 set) the births mask, MASK bit 1 = MP (the
+// multi-pass form; see life_stencil.h).
 #pragma once
 
 namespace gol {{
@@ -180,16 +184,17 @@ def main():
         if not m:
             continue
         key = tuple(int(x) for x in m.groups())
+        mp, key = key[5], key[:5]
         end = next(j for j in range(i + 1, len(lines)) if not lines[j].strip())
         # 2+ waves per SIMD when the kernel fits 256 registers (512 per SIMD lane)
-        want4 = vgprs.get(key, 0) <= 256 if vgprs else key[0] < 20
+        want4 = vgprs.get(key + (mp,), 0) <= 256 if vgprs else key[0] < 20
         for mask, frac, n in main_loop_fractions(lines[i:end], key[1] != 0):
-            kmask = key + (mask,)
+            kmask = key + (mask | (mp << 1),)
             good = frac if want4 else 1.0 - frac
             hot = key[1] in (0, 1) and key[0] >= 8
             ok = good >= 0.9
-            print(f"life_tb_kernel<{key[0]:2d}, {key[1]}, {key[2]}, {bool(key[3])}, {key[4]}> "
-                  f"{'masked' if mask else 'plain '} ({vgprs.get(key, '?')} regs): {n:5d} 8-byte instrs, "
+            print(f"life_tb_kernel<{key[0]:2d}, {key[1]}, {key[2]}, {bool(key[3])}, {key[4]}{', MP' if mp else ''}> "
+                  f"{'masked' if mask else 'plain '} ({vgprs.get(key + (mp,), '?')} regs): {n:5d} 8-byte instrs, "
                   f"{100 * good:3.0f}% at {'4' if want4 else '0'} mod 8, pad {int(kmask in pads)}"
                   f"{'' if ok else '  <- misplaced'}")
             if good < 0.35:  # a clear miss; ~50% means 4-byte code inside the compute

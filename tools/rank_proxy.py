@@ -85,6 +85,8 @@ def main():
     p.add_argument("--lib", default="", help="library build to load (GOL_LIB), dev A/B")
     p.add_argument("--transports", default="noop", help="noop and/or rccl (self-loop)")
     p.add_argument("--halo-depths", default="0", help="gol_config.halo_depth values (0 = auto)")
+    p.add_argument("--passes", default="1", help="GOL_DEV_PASSES values: passes per "
+                   "full-depth launch (1 = single-pass launches, 2-3 multi-pass)")
     p.add_argument("--shrinks", default="0", help="GOL_DEV_RANK_SHRINK values: 0 = one region "
                    "for the full-depth launches of a round (default), 1 = shrinking regions")
     a = p.parse_args()
@@ -99,19 +101,22 @@ def main():
         for trn in a.transports.split(","):
             for ov in (int(x) for x in a.overlaps.split(",")):
                 for hx in (int(x) for x in a.halo_depths.split(",")):
-                  for shr in a.shrinks.split(","):
-                    os.environ["GOL_DEV_RANK_SHRINK"] = shr
-                    for sk in a.skews.split(","):
-                        if sk == "auto":
-                            os.environ.pop("GOL_DEV_AGE_SKEW", None)
-                        else:
-                            os.environ["GOL_DEV_AGE_SKEW"] = sk
-                        e = rank_engine(pkg, n, rank, N, tp, a.handoff, ov, trn, hx)
-                        e.init_random(1)
-                        e.step(a.gens)
-                        e.sync()
-                        engines.append(((sk, ov, trn, shr), e, []))
+                    for shr in a.shrinks.split(","):
+                        os.environ["GOL_DEV_RANK_SHRINK"] = shr
+                        for npass in a.passes.split(","):
+                            os.environ["GOL_DEV_PASSES"] = npass
+                            for sk in a.skews.split(","):
+                                if sk == "auto":
+                                    os.environ.pop("GOL_DEV_AGE_SKEW", None)
+                                else:
+                                    os.environ["GOL_DEV_AGE_SKEW"] = sk
+                                e = rank_engine(pkg, n, rank, N, tp, a.handoff, ov, trn, hx)
+                                e.init_random(1)
+                                e.step(a.gens)
+                                e.sync()
+                                engines.append(((sk, ov, trn, shr), e, []))
         os.environ.pop("GOL_DEV_AGE_SKEW", None)
+        os.environ.pop("GOL_DEV_PASSES", None)
         os.environ.pop("GOL_DEV_RANK_SHRINK", None)
         for _ in range(a.rounds):
             for sk, e, ts in engines:
@@ -126,7 +131,7 @@ def main():
                               "halo_depth": e.halo_depth, "tb_depth": e.tb_depth,
                               "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
                               "age_skew": e.age_skew, "skew_cfg": sk[0], "overlap_cfg": sk[1],
-                              "transport": sk[2], "shrink_cfg": sk[3],
+                              "transport": sk[2], "shrink_cfg": sk[3], "passes": e.passes,
                               "autotune": list(e.tuning),
                               "rank_tcups": round(rate, 2),
                               "aggregate_tcups_if_balanced": round(rate * N, 1),
