@@ -58,6 +58,9 @@ struct StepArgs {
     int32_t npass;
     uint32_t shadow_off;
     uint32_t* mpflags;
+    // dev timing switches (GOL_DEV_MP_FLAGS; the field is not valid): 2 = no
+    // inter-pass waits, 8 = no shadow for the halo lanes
+    uint32_t mp_dev;
     const SegDesc* segs;  // device table
     int32_t nseg;
     int32_t strips;       // strip groups per row: ceil(ceil(wq / (L-2)) / (64/L))

@@ -637,6 +637,9 @@ void life_tb_kernel(StepArgs a)
     // from the table
     int64_t rb = pu ? pair_a : sg.out_lo + blk * a.rows_per_wave;
     int64_t rlen = pu ? pair_len : a.rows_per_wave;
+    // (multi-pass) the rows the strip's blocks cover as planned: only the bottom
+    // block may end past out_hi, clipped to a length of no hand-off class
+    int64_t planned_end = sg.out_lo + sg.nblk * a.rows_per_wave;
     if (a.rows_old && !pu) {
         const int32_t s = (int32_t)u_strip;
         const int64_t jo = min(sg.nblk, (int64_t)(a.units_old > s ? (uint32_t)(a.units_old - s + a.strips - 1) /
@@ -647,6 +650,7 @@ void life_tb_kernel(StepArgs a)
             rb = sg.out_lo + ny * a.rows_per_wave + (blk - ny) * a.rows_old;
             rlen = a.rows_old;
         }
+        planned_end = sg.out_lo + ny * a.rows_per_wave + jo * a.rows_old;
     }
     const int64_t re = min(rb + rlen, sg.out_hi);
     // step counts and indices are 32-bit (a block has at most rows_per_wave + 2K
@@ -663,6 +667,12 @@ void life_tb_kernel(StepArgs a)
     // buffer rows that are inside the buffer and the field (dead border)
     const int64_t vlo = max((int64_t)0, -sg.glob0), vhi = min(sg.in_rows, sg.field_h - sg.glob0);
     const bool has_above = blk > 0, has_below = blk < sg.nblk - 1;
+    // a clipped bottom block takes no hand-off in bottom-up passes (its length has
+    // no tail offset class, maybe not even an even one): it closes classically,
+    // and the block above it produces no side rows
+    const bool bottom_clipped = planned_end != sg.out_hi;
+    const bool up_consumer = has_above && !(bottom_clipped && blk == sg.nblk - 1);
+    const bool up_producer = has_below && !(bottom_clipped && blk == sg.nblk - 2);
 
     // Multi-pass launches (r05).  A launch runs `npass` passes of K generations
     // over the same row blocks, pass p reading buffer pbuf[p] and writing
@@ -698,6 +708,7 @@ void life_tb_kernel(StepArgs a)
     int64_t back_unit = 0;
     // one-shot flags of the multi-pass protocol: wait until *f is set, reset it
     auto mp_wait = [&](uint32_t* f) {
+        if (a.mp_dev & 2) return;  // dev timing: no inter-pass waits (field not valid)
         uint32_t v = 0;
         uint64_t w0 = 0;
         for (int it = 0;; ++it) {
@@ -747,11 +758,12 @@ void life_tb_kernel(StepArgs a)
         // (top-down: the block below, bottom-up: the block above) and produces them
         // for the block in front (pair units close their blocks the classic way:
         // their segment, the last of the launch, is one block deep)
-        producer = HAND && (up ? has_below : has_above);
-        consumer = HAND && (up ? has_above : has_below);
+        producer = HAND && (up ? up_producer : has_above);
+        consumer = HAND && (up ? up_consumer : has_below);
         // a consumer streams R + 2 input rows (steps < t_side), then side rows
         t_side = consumer ? (int32_t)(re - rb) + 2 : INT32_MAX;
-        s_back = (int32_t)(re - rb) + (consumer ? 0 : K);
+        // the first stream step beyond the block's far end (a consumer reads none)
+        s_back = consumer ? INT32_MAX : (int32_t)(re - rb) + K;
         const int64_t par = pass & 1;
         const int64_t prod = up ? unit + a.strips : unit - a.strips;  // a consumer's producer
         if constexpr (HAND) {
@@ -760,8 +772,8 @@ void life_tb_kernel(StepArgs a)
             my_flag = a.flags + par * a.total_units + unit;
             dn_flag = a.flags + par * a.total_units + prod;
         }
-        voff_ld = voff + ((pass > 0 && halo_lane) ? a.shadow_off : 0u);
-        const bool wr_shadow = pass < npass - 1 && halo_lane;
+        voff_ld = voff + ((pass > 0 && halo_lane && !(a.mp_dev & 8)) ? a.shadow_off : 0u);
+        const bool wr_shadow = pass < npass - 1 && halo_lane && !(a.mp_dev & 8);
         voff_st = voff + (wr_shadow ? a.shadow_off : 0u);
         st_ok = st_lane || wr_shadow;
         // rows another wavefront reads in the next pass go out write-through
@@ -769,7 +781,7 @@ void life_tb_kernel(StepArgs a)
         // the next pass's reader of this pass's head / done flags (see above)
         head_sent = !(pass < npass - 1 && (up ? has_below : has_above));
         done_need = pass < npass - 1 && (up ? has_above : has_below);
-        back_need = pass > 0 && (up ? has_above : has_below);
+        back_need = pass > 0 && !consumer && (up ? has_above : has_below);
         back_unit = up ? unit + a.strips : unit - a.strips;
         // the block in front's first rows of the previous pass
         if (pass > 0 && (up ? has_below : has_above))
@@ -903,6 +915,15 @@ void life_tb_kernel(StepArgs a)
         v = __builtin_amdgcn_readfirstlane(v);
         asm volatile("" : "+s"(v));
         return v;
+    };
+    // (multi-pass) write-through stores for the steps [t_first, t_last] of a
+    // non-final pass where they hold rows another wavefront reads next pass: the
+    // block's first and last K output rows (its other rows, and its halo lanes'
+    // shadow rows, only this wavefront reads back, through its own XCD's L2)
+    auto wt_for = [&](int32_t t_first, int32_t t_last) -> uint32_t {
+        if constexpr (!MP) return 0u;
+        const bool w = wt_stores && (t_first < 3 * K || t_last >= T - K);
+        return opaque(w ? 1u : 0u);
     };
     // (multi-pass) after the stores of the steps up to t_last: the head flag once
     // the block's first K output rows (steps 2K .. 3K-1) are out
@@ -1071,7 +1092,7 @@ void life_tb_kernel(StepArgs a)
             // previous block's stores) were issued a whole block of compute ago
             if constexpr (HAND) sync_point(t0);
         }
-        const uint32_t wt = MP ? opaque(wt_stores ? 1u : 0u) : 0u;
+        const uint32_t wt = wt_for(t0, t0 + kPrefetch - 1);
         if constexpr (MP && !kGuard) mp_sync(t0);
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) store(t0 + p, x[p], wt);
@@ -1152,7 +1173,7 @@ void life_tb_kernel(StepArgs a)
                         if (g >= 0 && g < K) x[p] = stage(g, p, t0 + p, x[p]);
                     }
                 }
-                const uint32_t wt = MP ? opaque(wt_stores ? 1u : 0u) : 0u;
+                const uint32_t wt = wt_for(t0, t0 + TOFF - 1);
 #pragma unroll
                 for (int p = 0; p < TOFF; ++p) store(t0 + p, x[p], wt);
                 if constexpr (MP) head_check(t0 + TOFF - 1);
@@ -1178,7 +1199,7 @@ void life_tb_kernel(StepArgs a)
                             x[p] = stage(g, p, tb + tau, x[p]);
                     }
                 }
-                const uint32_t wt = MP ? opaque(wt_stores ? 1u : 0u) : 0u;
+                const uint32_t wt = wt_for(tb + tau0, tb + tau0 + kPrefetch - 1);
 #pragma unroll
                 for (int p = 0; p < kPrefetch; ++p)
                     if (tau0 + p < kSideRows) store(tb + tau0 + p, x[p], wt);
