@@ -337,7 +337,7 @@ typedef struct gol_plan_summary {
     int64_t blocks;                 /* row blocks per strip (summed over segments) */
     int32_t handoff, tail_off;      /* hand-off blocks, their kernel's tail offset (-1) */
     uint32_t candidates;            /* autotuner variants built for this plan */
-    uint32_t reserved;
+    uint32_t passes;                /* passes per full-depth launch (gol_plan_passes) */
 } gol_plan_summary;
 gol_status gol_plan_model(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
                           int cus, int occ_classic, int occ_hand, gol_plan_summary* out);

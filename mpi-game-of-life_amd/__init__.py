@@ -93,7 +93,7 @@ class PlanSummary(ctypes.Structure):
         ("total_units", ctypes.c_int64), ("half_units", ctypes.c_int64),
         ("blocks", ctypes.c_int64),
         ("handoff", ctypes.c_int32), ("tail_off", ctypes.c_int32),
-        ("candidates", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+        ("candidates", ctypes.c_uint32), ("passes", ctypes.c_uint32),
     ]
 
 

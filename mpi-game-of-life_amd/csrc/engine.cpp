@@ -1260,6 +1260,7 @@ void step_schedule(uint32_t K, uint64_t Hx, bool overlap, bool halo_fresh, uint6
 }
 
 gol_status plan_resident(gol_engine* e, const gol_config* cfg);
+void decide_passes(gol_engine* e, size_t words);
 gol_status autotune_plans(gol_engine* e);
 void resolve_aliases(gol_engine* e);
 
@@ -1414,17 +1415,7 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
     GOL_TRY(raw_regions(e, h, cfg, geom, raw));
 
     const size_t words = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
-    // Multi-pass launches (GOL_DEV_PASSES = 2 or 3; life_stencil.h): single-GPU
-    // engines alone on their device and rank engines, fields whose shadow offset
-    // fits the kernel's 32-bit lane offsets, depths whose P K outer halo columns
-    // stay inside the halo lane (P K < 64)
-    if (const char* v = std::getenv("GOL_DEV_PASSES")) {
-        const int np = std::atoi(v);
-        if (np >= 2 && np <= 3 && !e->shared_device && np * (int)e->K < 64 &&
-            gol::multipass_kernel_exists((int)e->K, e->rule, e->planes) &&
-            (words + e->stride) * sizeof(uint64_t) < (1ull << 32))
-            e->npass = (uint32_t)np;
-    }
+    decide_passes(e, words);
     const size_t halves = e->npass > 1 ? 2 : 1;
     e->nbuf = e->npass > 1 ? 4 : 2;
     e->shadow_off = e->npass > 1 ? (uint32_t)(words * sizeof(uint64_t)) : 0u;
@@ -1687,6 +1678,22 @@ gol_status step_resident(gol_engine* e, uint64_t generations)
 
 // `passes` > 1: a multi-pass launch of that many depth-K passes (plans with npass
 // >= passes), reading buf[cur] and writing buf[cur + 1 .. cur + passes]
+// Multi-pass launches (GOL_DEV_PASSES = 2 or 3; life_stencil.h, measured slower
+// than single-pass launches in r05): single-GPU engines alone on their
+// device and rank engines, fields whose shadow offset fits the kernel's 32-bit
+// lane offsets (`words` per buffer), depths whose P K outer halo columns stay
+// inside the halo lane (P K < 64)
+void decide_passes(gol_engine* e, size_t words)
+{
+    if (const char* v = std::getenv("GOL_DEV_PASSES")) {
+        const int np = std::atoi(v);
+        if (np >= 2 && np <= 3 && !e->shared_device && np * (int)e->K < 64 &&
+            gol::multipass_kernel_exists((int)e->K, e->rule, e->planes) &&
+            (words + e->stride) * sizeof(uint64_t) < (1ull << 32))
+            e->npass = (uint32_t)np;
+    }
+}
+
 gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
                   hipStream_t stream = nullptr, int passes = 1)
 {
@@ -2190,6 +2197,7 @@ gol_status gol_plan_model(uint64_t h, uint64_t w, const gol_config* cfg, int ran
     GOL_TRY(host_layout(e.get(), h, w, &c));
     std::vector<std::vector<SegDesc>> raw;
     GOL_TRY(raw_regions(e.get(), h, &c, nranks > 1 ? &g : nullptr, raw));
+    decide_passes(e.get(), (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride);
     GOL_TRY(build_plans(e.get(), raw));
     if (e->plans.empty()) return fail(GOL_ESTATE, "no launch plan");
     const size_t pi = nranks > 1 ? std::min<size_t>(e->plans.size() - 1, e->K - 1) : 0;
@@ -2210,6 +2218,7 @@ gol_status gol_plan_model(uint64_t h, uint64_t w, const gol_config* cfg, int ran
     for (const auto& sg : p.segs) out->blocks += sg.nblk;
     out->handoff = (p.hand && p.multi_blk) ? 1 : 0;
     out->tail_off = out->handoff ? gol::handoff_toff(p.rpw, (int)e->K, e->planes) : -1;
+    out->passes = (uint32_t)p.npass;
     out->candidates = pi < e->plan_alts.size() ? (uint32_t)e->plan_alts[pi].size() : 0u;
     return GOL_OK;
 }

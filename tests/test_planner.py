@@ -163,3 +163,22 @@ def test_plan_model_rejects_bad_args(pkg):
         pkg.plan_model(100, 100, rank=1, nranks=1)
     with pytest.raises(pkg.GolError):
         pkg.plan_model(10, 100, rank=0, nranks=20)
+
+
+@pytest.mark.parametrize("passes", [2, 3])
+@pytest.mark.parametrize("h,rank,n", [(65536, 4, 8), (65536, 2, 4), (8416, 0, 1), (3007, 0, 1)])
+def test_multipass_plans(pkg, monkeypatch, passes, h, rank, n):
+    """Multi-pass launches (GOL_DEV_PASSES, life_stencil.h): every wavefront
+    waits for its row neighbours between passes, so the plan must be one round
+    of the occupancy, one segment, and without the half strip (its pair units
+    have no pass protocol)."""
+    monkeypatch.setenv("GOL_DEV_PASSES", str(passes))
+    p = pkg.plan_model(h, 65536, rank=rank, nranks=n, tb_depth=16)
+    check_plan(p)
+    assert p["passes"] == passes
+    assert p["half_units"] == 0
+    assert p["total_units"] <= OCC * 4 * CUS
+    # no multi-pass kernel at depth 8 (multipass_kernel_exists)
+    assert pkg.plan_model(h, 65536, rank=rank, nranks=n, tb_depth=8)["passes"] == 1
+    monkeypatch.delenv("GOL_DEV_PASSES")
+    assert pkg.plan_model(h, 65536, rank=rank, nranks=n, tb_depth=16)["passes"] == 1
