@@ -1705,8 +1705,11 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
     StepArgs a{};
     for (int i = 0; i <= passes; ++i) a.pbuf[i] = e->buf[(e->cur + i) % e->nbuf];
     a.npass = passes;
+#if GOL_EXP
+    // (timing-only switches that invalidate the field: experimental builds only)
     if (passes > 1)
         if (const char* v = std::getenv("GOL_DEV_MP_FLAGS")) a.mp_dev = (uint32_t)std::atoi(v);
+#endif
     a.shadow_off = e->shadow_off;
     a.mpflags = e->mpflags;
     a.err = e->d_err;

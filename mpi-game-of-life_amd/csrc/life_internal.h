@@ -58,7 +58,7 @@ struct StepArgs {
     int32_t npass;
     uint32_t shadow_off;
     uint32_t* mpflags;
-    // dev timing switches (GOL_DEV_MP_FLAGS; the field is not valid): 2 = no
+    // dev timing switches (GOL_DEV_MP_FLAGS, GOL_EXP builds; the field is not valid): 2 = no
     // inter-pass waits, 8 = no shadow for the halo lanes
     uint32_t mp_dev;
     const SegDesc* segs;  // device table
