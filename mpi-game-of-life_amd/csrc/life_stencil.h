@@ -176,6 +176,24 @@ __device__ __forceinline__ Grp<NP> load_field(const uint64_t* p)
 #endif
 }
 
+// Dev A/B (GOL_NT_WARM=1): non-temporal loads for the warm-up rows loaded up front
+// only (the start burst), the steady stream allocating as usual.
+#ifndef GOL_NT_WARM
+#define GOL_NT_WARM 0
+#endif
+template <int NP>
+__device__ __forceinline__ Grp<NP> load_warm(const uint64_t* p)
+{
+#if GOL_NT_WARM
+    Grp<NP> g;
+#pragma unroll
+    for (int i = 0; i < NP / 2; ++i) g.w[i] = __builtin_nontemporal_load(p + i);
+    return g;
+#else
+    return load_field<NP>(p);
+#endif
+}
+
 template <int NP>
 __device__ __forceinline__ void store_side(uint64_t* p, const Pl<NP>& x)
 {
@@ -489,6 +507,12 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 #ifndef GOL_WARM_PREFETCH
 #define GOL_WARM_PREFETCH 1
 #endif
+#ifndef GOL_WARM_AHEAD
+#define GOL_WARM_AHEAD 0  // 0: every warm-up row up front
+#endif
+#ifndef GOL_WARM_BARRIER
+#define GOL_WARM_BARRIER 0
+#endif
 
 // MP: the multi-pass form (StepArgs::npass > 1; a separate instantiation, so the
 // single-pass kernel's steady loop stays exactly as it was)
@@ -507,6 +531,8 @@ void life_tb_kernel(StepArgs a)
     constexpr int kPrefetch = kPfOf<NP, K>();
     constexpr int kSideRows = 2 * (K - 1);  // hand-off rows per block: 2 per generation 1..K-1
     constexpr int kWarmSteps = (2 * K + kPrefetch - 1) / kPrefetch * kPrefetch;  // unrolled warm-up
+    constexpr int kWarmAhead =
+        (GOL_WARM_AHEAD > 0 && GOL_WARM_AHEAD < kWarmSteps) ? GOL_WARM_AHEAD : kWarmSteps;
     static_assert(K + 2 * kPrefetch <= kGuardRows, "streaming loads must stay in the guard rows");
     static_assert(!HAND || K >= kHandoffMinDepth, "hand-off kernels start at kHandoffMinDepth");
     static_assert(TOFF >= 0 && TOFF < kPrefetch && (HAND || TOFF == 0), "tail offset");
@@ -814,10 +840,12 @@ void life_tb_kernel(StepArgs a)
     // its issue: a chain of HBM round trips (s_waitcnt vmcnt(0/1) after each
     // load) that made the 2K warm-up steps take 16-20 us per wavefront at every
     // shape (profiles/r05/wave_phases_*.jsonl).
+    // (dev A/B, GOL_WARM_AHEAD = n: only the first n warm-up rows up front, each
+    // warm-up block issuing the rows n steps ahead of it)
     Grp<NP> wring[kWarmSteps];
 #pragma unroll
-    for (int p = 0; p < kWarmSteps; ++p)  // (input rows: t_side >= warm-up + 2 blocks)
-        wring[p] = load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)p * rs + voff_ld));
+    for (int p = 0; p < kWarmAhead; ++p)  // (input rows: t_side >= warm-up + 2 blocks)
+        wring[p] = load_warm<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)p * rs + voff_ld));
     constexpr int kSteadyIssue = kWarmSteps >= 2 * kPrefetch ? kWarmSteps - 2 * kPrefetch : 0;
 #else
 #pragma unroll
@@ -1003,10 +1031,13 @@ void life_tb_kernel(StepArgs a)
         constexpr bool kMask = kBirths && kMode != kPure;
         Pl<NP> x[kPrefetch];
 #if GOL_WARM_PREFETCH
+        if constexpr (kGuard && GOL_WARM_BARRIER) __builtin_amdgcn_sched_barrier(0);
         if constexpr (kGuard) {
 #pragma unroll
             for (int p = 0; p < kPrefetch; ++p) {
                 x[p] = ingest(t0 + p, wring[t0 + p], std::false_type{});
+                if (t0 + kWarmAhead + p < kWarmSteps)
+                    wring[t0 + kWarmAhead + p] = load_in(t0 + kWarmAhead + p);
                 if (t0 == kSteadyIssue) ring[p] = load_in(kWarmSteps + p);
             }
         } else
