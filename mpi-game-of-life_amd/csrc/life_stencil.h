@@ -507,11 +507,21 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 #ifndef GOL_WARM_PREFETCH
 #define GOL_WARM_PREFETCH 1
 #endif
+// (r05) The warm-up's first GOL_WARM_AHEAD rows are loaded up front and each
+// warm-up block issues the rows that many steps ahead of it, with a scheduling
+// barrier between the blocks that keeps those loads where they are.  Every
+// wavefront of a launch starts at once and its first loads stall at issue on the
+// CU's outstanding requests (the start burst): with 16 rows up front
+// instead of all 32 the first blocks compute while the rest of the rows stream
+// in.  RCCL per-rank proxy, builds alternating in their own processes on one box
+// (profiles/r05/ab_warm_ahead.jsonl), TCUPS: 8-way 118.7 -> 121.1 and 117.1 ->
+// 118.0 (two boxes), 4-way 134.7 -> 136.6 and 134.6 -> 136.0, 2-way 146.5 ->
+// 147.8; 65536^2 unchanged (157.1-157.4).  0 = every warm-up row up front.
 #ifndef GOL_WARM_AHEAD
-#define GOL_WARM_AHEAD 0  // 0: every warm-up row up front
+#define GOL_WARM_AHEAD 16
 #endif
 #ifndef GOL_WARM_BARRIER
-#define GOL_WARM_BARRIER 0
+#define GOL_WARM_BARRIER 1
 #endif
 
 // MP: the multi-pass form (StepArgs::npass > 1; a separate instantiation, so the
