@@ -511,14 +511,15 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 // warm-up block issues the rows that many steps ahead of it, with a scheduling
 // barrier between the blocks that keeps those loads where they are.  Every
 // wavefront of a launch starts at once and its first loads stall at issue on the
-// CU's outstanding requests (the start burst): with 16 rows up front
-// instead of all 32 the first blocks compute while the rest of the rows stream
-// in.  RCCL per-rank proxy, builds alternating in their own processes on one box
-// (profiles/r05/ab_warm_ahead.jsonl), TCUPS: 8-way 118.7 -> 121.1 and 117.1 ->
-// 118.0 (two boxes), 4-way 134.7 -> 136.6 and 134.6 -> 136.0, 2-way 146.5 ->
-// 147.8; 65536^2 unchanged (157.1-157.4).  0 = every warm-up row up front.
+// CU's outstanding requests (the start burst): with one block of rows
+// up front instead of all 32 the first blocks compute while the rest stream in.
+// RCCL per-rank proxy, 5 runs with the build order rotated, one box
+// (profiles/r05/ab_warm_ahead.jsonl), mean TCUPS of own rows, all 32 rows up
+// front / 16 / 12 / 8 ahead: 8-way 117.8 / 118.4-118.9 / 118.9 / 119.7, 4-way
+// 136.0 / 136.1-136.4 / 137.1 / 136.8; 65536^2 157.8-158.0 (16) vs 158.1-158.2
+// (8).  0 = every warm-up row up front.
 #ifndef GOL_WARM_AHEAD
-#define GOL_WARM_AHEAD 16
+#define GOL_WARM_AHEAD 8
 #endif
 #ifndef GOL_WARM_BARRIER
 #define GOL_WARM_BARRIER 1
