@@ -549,7 +549,8 @@ RowPlan pick_rows_per_wave(const std::vector<SegDesc>& segs, uint64_t wq, int K,
 // get longer blocks: the bottom blocks of each strip whose units are < units_old
 // have rows_old rows, the others rows_young, with the young/old rate ratio rho of
 // the block kind (kAgeRate*; the in-process A/B optimum, profiles/r02/ab_skew*.jsonl).
-// GOL_DEV_AGE_SKEW overrides rho (dev A/B; 0 turns the skew off).
+// GOL_DEV_AGE_SKEW overrides rho (dev A/B; 0 turns the skew off),
+// GOL_DEV_AGE_SKEW_HAND the hand-off blocks' rho only.
 constexpr double kAgeRateHand = 0.78, kAgeRateClassic = 0.72;
 
 constexpr double kHandSkewCost = 1.05;
@@ -569,6 +570,8 @@ Skew age_skew(const SegDesc& sg, int64_t R, int32_t strips, int64_t units_old, i
     Skew best_s;
     double rho = hand ? kAgeRateHand : kAgeRateClassic;
     if (const char* v = std::getenv("GOL_DEV_AGE_SKEW")) rho = std::atof(v);
+    if (hand)
+        if (const char* v = std::getenv("GOL_DEV_AGE_SKEW_HAND")) rho = std::atof(v);
     rho *= rho_mult;
     const int64_t rows = sg.out_hi - sg.out_lo;
     if (rho <= 0 || rho >= 1 || occ != 2 || rows <= 0) return best_s;
