@@ -727,7 +727,9 @@ void life_tb_kernel(StepArgs a)
     // bytes on): after P passes of K generations their outer P*K columns are wrong
     // and the exact lanes beside them still see exact columns (P*K <= 48 < 64).
     // The stencil is symmetric under a vertical flip, so a bottom-up pass is the
-    // same code on rows addressed with a negative stride.
+    // same code on rows addressed with a negative stride.  (Measured slower than
+    // single-pass launches: the extra per-pass state spills the hand-off kernels
+    // and lengthens the address arithmetic; a dev switch, GOL_DEV_PASSES)
     const int npass = MP ? a.npass : 1;
     const bool halo_lane = qin && !exact && !pu;
     bool up = false, producer = false, consumer = false, head_sent = false;
