@@ -859,7 +859,13 @@ void life_tb_kernel(StepArgs a)
 #pragma unroll
     for (int p = 0; p < kWarmAhead; ++p)  // (input rows: t_side >= warm-up + 2 blocks)
         wring[p] = load_warm<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)p * rs + voff_ld));
-    constexpr int kSteadyIssue = kWarmSteps >= 2 * kPrefetch ? kWarmSteps - 2 * kPrefetch : 0;
+    // (the steady ring's first rows: issued GOL_STEADY_LEAD warm-up blocks before the
+    // steady loop; dev A/B)
+#ifndef GOL_STEADY_LEAD
+#define GOL_STEADY_LEAD 2
+#endif
+    constexpr int kSteadyIssue =
+        kWarmSteps >= GOL_STEADY_LEAD * kPrefetch ? kWarmSteps - GOL_STEADY_LEAD * kPrefetch : 0;
 #else
 #pragma unroll
     for (int p = 0; p < kPrefetch; ++p) ring[p] = load_step(p);
