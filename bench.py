@@ -12,8 +12,10 @@ RCCL halo exchanges (strong scaling: total work fixed).
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Timed region: W untimed steps, then barrier + device sync, K steps, device sync
-+ barrier; max over ranks.  The field is resident in HBM throughout.  Rank 0
-prints one JSON line.
++ barrier; max over ranks.  No HIP events are recorded inside it (r06); K more
+steps with sampled launch events follow it and give the launch durations
+(`roofline`) and the per-rank breakdown.  The field is resident in HBM
+throughout.  Rank 0 prints one JSON line.
 
 `roofline` names the bound that binds.  The stencil kernel is temporally blocked
 (K = 16 generations per launch) and VALU-issue bound, not HBM bound (DESIGN.md
@@ -285,40 +287,59 @@ def rccl_selfcheck(pkg, dist, torch, world, rank, local, handoff=0):
 
 
 def timed_steps(eng, gens, steps, warmup, world, dist, torch, timing_every=8):
-    """W untimed steps, then K steps between barrier + device sync brackets; HIP
-    events around every `timing_every`-th launch.  Returns (seconds, timing)."""
+    """W untimed steps, then K steps between barrier + device sync brackets with
+    no events on the streams (single-stream engines replay their hipGraph): the
+    measured time.  Then K more steps with HIP events around every
+    `timing_every`-th launch (and, on rank engines, every halo round and
+    exchange): the launch durations and the per-rank breakdown.  Returns
+    (seconds, seconds of the event pass, timing of the event pass)."""
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def region():
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.step(gens)
+        eng.sync()
+        torch.cuda.synchronize()
+        barrier()
+        return time.perf_counter() - t0
     for _ in range(warmup):
         eng.step(gens)
     eng.sync()
+    eng.set_timing(0)
+    dt = region()
     eng.set_timing(timing_every)
     eng.reset_timing()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        eng.step(gens)
-    eng.sync()
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    return dt, eng.timing()
+    dt_ev = region()
+    tm = eng.timing()
+    eng.set_timing(0)
+    return dt, dt_ev, tm
 
 
 def rank_breakdown(eng, tm, dt, steps, rank):
-    """(r05) Where one rank's step time goes, from its own timing (N > 1): the
-    stencil launches (mean HIP-event duration of the sampled launches x every
-    launch issued), the halo exchanges (HIP events around each one on its stream;
-    RCCL's stream time includes waiting for the peers), and the rest (launch gaps,
-    host work, the max-over-ranks barrier is not in it).  Rounds per step = the
-    exchanges; rows per launch = the buffer rows a full-depth launch computes
-    (own rows + 2 Hx - 2 K with the shared region, engine.cpp rank_geometry)."""
+    """Where one rank's step time goes, from its own HIP events (N > 1), as
+    measured spans that add up to ms_per_step in both exchange modes (r06):
+      kernel_span: each halo round's compute-stream span, from before its first
+        launch to after its last (band stream joined), summed (launch gaps
+        inside a round included);
+      exchange: the halo exchanges' own stream time (RCCL's includes waiting for
+        the peers), split into exchange_exposed (outside the round spans: all of
+        a blocking exchange, the tail of an overlapped one past its round's end)
+        and exchange_hidden (the rest, under the interior launch);
+      other = ms_per_step - kernel_span - exchange_exposed: host work and gaps
+        between rounds (the max-over-ranks barrier is not in it).
+    avg_launch_ms: the mean sampled launch (overlapped band and interior launches
+    run concurrently, so launches x mean is not a time share).  Rows per launch =
+    the buffer rows a full-depth launch computes (engine.cpp rank_geometry)."""
     launches = max(tm["launches"], 1)
     avg = tm["kernel_ms"] / launches
-    kern = avg * tm["launches_issued"] / steps
+    span = tm["round_ms"] / steps
     xch = tm["exchange_ms"] / steps
+    exposed = tm["exchange_exposed_ms"] / steps
     ms = dt / steps * 1e3
     return {
         "rank": rank, "own_rows": eng.rows, "row0": eng.row0, "halo_depth": eng.halo_depth,
@@ -330,10 +351,13 @@ def rank_breakdown(eng, tm, dt, steps, rank):
         "avg_launch_ms": round(avg, 4),
         "own_tcups_per_launch": round(eng.rows * eng.w * eng.tb_depth / (avg * 1e-3) / 1e12, 2)
         if avg > 0 else None,
-        "kernel_ms_per_step": round(kern, 3),
+        "rounds_per_step": round(tm["rounds"] / steps, 2),
+        "kernel_span_ms_per_step": round(span, 3),
         "exchanges_per_step": round(tm["exchanges"] / steps, 2),
         "exchange_ms_per_step": round(xch, 3),
-        "other_ms_per_step": round(ms - kern - xch, 3),
+        "exchange_exposed_ms_per_step": round(exposed, 3),
+        "exchange_hidden_ms_per_step": round(xch - exposed, 3),
+        "other_ms_per_step": round(ms - span - exposed, 3),
     }
 
 
@@ -356,7 +380,7 @@ def sub_record(pkg, torch, local, size, rule, gens, steps, warmup, seed):
     r = pkg.REF_RULE if rule == "ref" else pkg.CONWAY
     with pkg.Engine(size, size, rule=r, device=local) as eng:
         eng.init_random(seed)
-        dt, tm = timed_steps(eng, gens, steps, warmup, 1, None, torch)
+        dt, _, tm = timed_steps(eng, gens, steps, warmup, 1, None, torch)
         frac, work = valu_frac(tm, rule)
         return {
             "workload": f"{size}x{size}, {gens} generations per step, "
@@ -436,9 +460,9 @@ def main():
         # blocking one: the same K steps, reported beside `value`
         eng = rank_engine(2)
         eng.init_random(a.seed)
-        ov_dt, ov_tm = timed_steps(eng, a.gens, a.steps, a.warmup, world, dist, torch, 8)
+        ov_dt, ov_dt_ev, ov_tm = timed_steps(eng, a.gens, a.steps, a.warmup, world, dist, torch, 8)
         ov_per = [None] * world
-        dist.all_gather_object(ov_per, rank_breakdown(eng, ov_tm, ov_dt, a.steps, rank))
+        dist.all_gather_object(ov_per, rank_breakdown(eng, ov_tm, ov_dt_ev, a.steps, rank))
         ov_dt = max_over_ranks(ov_dt)
         eng.close()
         modes = {"overlapped": {"value": round(float(n) * n * a.gens * a.steps / ov_dt / 1e9, 2),
@@ -450,27 +474,16 @@ def main():
         selfcheck = None
     eng.init_random(a.seed)
 
-    # HIP events around every 8th launch: representative launch durations without
-    # the per-event stream cost (~6 us) landing on every launch of the timed region
-    dt, tm = timed_steps(eng, a.gens, a.steps, a.warmup, world, dist, torch, 8)
-    # The events above keep a single-stream engine off its hipGraph replay (the
-    # default path without timing): one more step on that path, not part of
-    # `value`, shows the two agree
+    # the timed region runs without events; a second pass of K steps with HIP
+    # events around every 8th launch (representative launch durations without the
+    # per-event stream cost, ~6 us, on every launch) gives the launch times, the
+    # roofline and the per-rank breakdown
+    dt, dt_ev, tm = timed_steps(eng, a.gens, a.steps, a.warmup, world, dist, torch, 8)
     per_rank = None
     if world > 1:
         per_rank = [None] * world
-        dist.all_gather_object(per_rank, rank_breakdown(eng, tm, dt, a.steps, rank))
-    eng.set_timing(0)
-    barrier()
-    dt_graph = 1e30
-    for _ in range(2):  # a step count of odd launch parity alternates 2 captured graphs
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        eng.step(a.gens)
-        eng.sync()
-        torch.cuda.synchronize()
-        dt_graph = min(dt_graph, time.perf_counter() - t1)
-    barrier()
+        dist.all_gather_object(per_rank, rank_breakdown(eng, tm, dt_ev, a.steps, rank))
+    dt_ev = max_over_ranks(dt_ev)
     dt = max_over_ranks(dt)
     avg_launch_ms = max_over_ranks(tm["kernel_ms"] / max(tm["launches"], 1))
 
@@ -521,7 +534,8 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3),
-            "ms_per_step_untimed_path": round(dt_graph * 1e3, 3),
+            # the same K steps with HIP events on the streams (the launch timing pass)
+            "ms_per_step_event_pass": round(dt_ev / a.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,

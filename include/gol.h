@@ -122,7 +122,12 @@ typedef struct gol_timing {
                                   halo stage-rows of classic blocks and the
                                   strips' halo lanes */
     uint32_t streams;      /* stripe streams whose launches run concurrently */
-    uint32_t reserved;
+    /* (r06; `reserved` before) in: the caller's sizeof(gol_timing).  The layout
+     * grew in r05 and r06; gol_get_timing writes the whole struct only when this
+     * equals the library's sizeof(gol_timing), else only the r04 fields above
+     * (40 bytes), so a caller built against an older header is never overrun.
+     * out: the bytes written. */
+    uint32_t struct_size;
     /* (r05) while timing is on: every stencil launch issued (sampled or not) and
      * the buffer rows the sampled launches computed; rank engines also time
      * every halo exchange with HIP events on its stream (RCCL: the stream time
@@ -132,7 +137,18 @@ typedef struct gol_timing {
     double launch_rows;
     uint64_t exchanges;
     double exchange_ms;
+    /* (r06) rank engines while timing is on: `rounds` halo rounds, round_ms = the
+     * sum of their compute-stream spans (HIP events before the round's first
+     * launch and after its last, the band stream joined), exchange_exposed_ms =
+     * the part of the exchanges outside those spans (a blocking exchange: all of
+     * it; an overlapped one: what runs past the end of its round's span).  Per
+     * step: round_ms + exchange_exposed_ms <= the wall time; the rest is host
+     * work and launch gaps between rounds. */
+    uint64_t rounds;
+    double round_ms;
+    double exchange_exposed_ms;
 } gol_timing;
+#define GOL_TIMING_R04_BYTES 40u
 
 /* Defaults: reference-effective rule, GLOBAL semantics, auto tuning. */
 void gol_config_init(gol_config* cfg);

@@ -74,11 +74,14 @@ class Timing(ctypes.Structure):
         ("cell_gens", ctypes.c_double),
         ("cell_gens_computed", ctypes.c_double),
         ("streams", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("struct_size", ctypes.c_uint32),  # in: sizeof(gol_timing) (gol.h)
         ("launches_issued", ctypes.c_uint64),
         ("launch_rows", ctypes.c_double),
         ("exchanges", ctypes.c_uint64),
         ("exchange_ms", ctypes.c_double),
+        ("rounds", ctypes.c_uint64),
+        ("round_ms", ctypes.c_double),
+        ("exchange_exposed_ms", ctypes.c_double),
     ]
 
 
@@ -410,12 +413,12 @@ class Engine:
         _check(lib().gol_reset_timing(self._h))
 
     def timing(self):
-        t = Timing()
+        t = Timing(struct_size=ctypes.sizeof(Timing))
         _check(lib().gol_get_timing(self._h, ctypes.byref(t)))
-        return {"launches": t.launches, "kernel_ms": t.kernel_ms, "cell_gens": t.cell_gens,
-                "cell_gens_computed": t.cell_gens_computed, "streams": t.streams,
-                "launches_issued": t.launches_issued, "launch_rows": t.launch_rows,
-                "exchanges": t.exchanges, "exchange_ms": t.exchange_ms}
+        if t.struct_size != ctypes.sizeof(Timing):
+            raise GolError(GOL_ESTATE, f"libgol.so's gol_timing is {t.struct_size} bytes, "
+                                       f"this binding's {ctypes.sizeof(Timing)}")
+        return {k: getattr(t, k) for k, _ in Timing._fields_ if k != "struct_size"}
 
 
 def _make_transport(fn):

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -324,6 +325,14 @@ struct gol_engine {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
     std::vector<double> pending_cells, pending_cells_comp, pending_rows;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_xpending;  // exchanges
+    std::vector<char> xpending_blocking;  // ... on the compute stream (1) or comm (0)
+    // rank engines, per round: the compute stream's span from before the round's
+    // first launch to after its last (band launch joined), and the end of the
+    // overlapped exchange issued in that round (null when it blocks)
+    struct RoundEv {
+        hipEvent_t start, end, xend;
+    };
+    std::vector<RoundEv> ev_rpending;
     gol_timing tm{};
 };
 
@@ -1492,17 +1501,45 @@ gol_status flush_timing(gol_engine* e)
         e->ev_free.push_back(p.first);
         e->ev_free.push_back(p.second);
     }
-    for (auto& p : e->ev_xpending) {
+    // an overlapped exchange is exposed for the part that ends after its round's
+    // compute span (the next round's launches wait for it); a blocking one sits
+    // between two rounds on the compute stream, all of it exposed
+    std::map<hipEvent_t, float> round_end_to_xend;
+    for (auto& r : e->ev_rpending) {
+        HIP_TRY(hipEventSynchronize(r.end));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, r.start, r.end));
+        e->tm.rounds += 1;
+        e->tm.round_ms += ms;
+        if (r.xend) {
+            HIP_TRY(hipEventSynchronize(r.xend));
+            float tail = 0.f;
+            HIP_TRY(hipEventElapsedTime(&tail, r.end, r.xend));
+            round_end_to_xend[r.xend] = tail;
+        }
+        e->ev_free.push_back(r.start);
+        e->ev_free.push_back(r.end);
+    }
+    for (size_t i = 0; i < e->ev_xpending.size(); ++i) {
+        auto& p = e->ev_xpending[i];
         HIP_TRY(hipEventSynchronize(p.second));
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, p.first, p.second));
         e->tm.exchanges += 1;
         e->tm.exchange_ms += ms;
+        float exposed = ms;
+        if (!e->xpending_blocking[i]) {
+            auto it = round_end_to_xend.find(p.second);
+            exposed = it == round_end_to_xend.end() ? ms : std::min(ms, std::max(0.f, it->second));
+        }
+        e->tm.exchange_exposed_ms += exposed;
         e->ev_free.push_back(p.first);
         e->ev_free.push_back(p.second);
     }
     e->ev_pending.clear();
     e->ev_xpending.clear();
+    e->xpending_blocking.clear();
+    e->ev_rpending.clear();
     e->pending_cells.clear();
     e->pending_cells_comp.clear();
     e->pending_rows.clear();
@@ -1688,9 +1725,11 @@ gol_status step_resident(gol_engine* e, uint64_t generations)
 // inside the halo lane (P K < 64)
 void decide_passes(gol_engine* e, size_t words)
 {
+    if (!gol::kDevKernels) return;  // multi-pass kernels: dev build only
     if (const char* v = std::getenv("GOL_DEV_PASSES")) {
         const int np = std::atoi(v);
-        if (np >= 2 && np <= 3 && !e->shared_device && np * (int)e->K < 64 &&
+        // (group members launch single-pass: gol_group_step runs each launch op)
+        if (np >= 2 && np <= 3 && !e->shared_device && !e->grouped && np * (int)e->K < 64 &&
             gol::multipass_kernel_exists((int)e->K, e->rule, e->planes) &&
             (words + e->stride) * sizeof(uint64_t) < (1ull << 32))
             e->npass = (uint32_t)np;
@@ -1960,6 +1999,7 @@ gol_status exchange(gol_engine* e, hipStream_t st)
     GOL_TRY(exchange_body(e, st));
     HIP_TRY(hipEventRecord(e1, st));
     e->ev_xpending.push_back({e0, e1});
+    e->xpending_blocking.push_back(st == e->stream ? 1 : 0);
     return GOL_OK;
 }
 
@@ -2254,6 +2294,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     e->R = g.R;
     e->Hx = g.Hx;
     e->shared_device = shared_device;
+    e->grouped = group && nranks > 1;  // (decide_passes reads it in init_common)
     // stripe engines run the streaming kernel even as the only rank, so that
     // gol_round_schedule (host-only: no occupancy query for the resident plan)
     // lists exactly the launches gol_step runs
@@ -2449,9 +2490,14 @@ void gol_destroy(gol_engine* e)
     for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second.exec);
     if (e->d_acc) (void)hipFree(e->d_acc);
     if (e->d_flag) (void)hipFree(e->d_flag);
-    for (auto& p : e->ev_pending) {
-        (void)hipEventDestroy(p.first);
-        (void)hipEventDestroy(p.second);
+    for (const auto* pend : {&e->ev_pending, &e->ev_xpending})
+        for (auto& p : *pend) {
+            (void)hipEventDestroy(p.first);
+            (void)hipEventDestroy(p.second);
+        }
+    for (auto& r : e->ev_rpending) {  // (xend belongs to ev_xpending)
+        (void)hipEventDestroy(r.start);
+        (void)hipEventDestroy(r.end);
     }
     for (auto ev : e->ev_free) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -2837,8 +2883,31 @@ gol_status gol_step(gol_engine* e, uint64_t generations)
     // consecutive full-depth launch ops of one block plan (the shared region of a
     // round, rank_geometry) run as one multi-pass launch when the plan has passes
     auto root = [e](int pi) { return e->plan_alias[(size_t)pi] >= 0 ? e->plan_alias[(size_t)pi] : pi; };
+    // timing on: each round's compute span (after its exchange op, to after its
+    // last launch with the band stream joined) for the per-rank breakdown
+    gol_engine::RoundEv rev{nullptr, nullptr, nullptr};
+    auto close_round = [e, &rev]() -> gol_status {
+        if (!rev.start) return GOL_OK;
+        if (e->band_stream) {
+            HIP_TRY(hipEventRecord(e->ev_join, e->band_stream));
+            HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
+        }
+        GOL_TRY(get_event(e, &rev.end));
+        HIP_TRY(hipEventRecord(rev.end, e->stream));
+        e->ev_rpending.push_back(rev);
+        rev = {nullptr, nullptr, nullptr};
+        return GOL_OK;
+    };
     for (size_t i = 0; i < ops.size(); ++i) {
         const SchedOp& op = ops[i];
+        if (e->timing_every && (op.kind == GOL_OP_EXCHANGE || op.kind == GOL_OP_WAIT_EXCHANGE))
+            GOL_TRY(close_round());
+        if (e->timing_every && op.kind == GOL_OP_EXCHANGE_ASYNC && rev.start) {
+            // the round's overlapped exchange: its end event is the one exchange() records
+            GOL_TRY(run_launch_op(e, op, xchg));
+            rev.xend = e->ev_xpending.empty() ? nullptr : e->ev_xpending.back().second;
+            continue;
+        }
         if (op.kind == GOL_OP_LAUNCH && op.depth == e->K && e->plans[(size_t)op.plan].npass > 1) {
             int n = 1;
             while (n < e->plans[(size_t)op.plan].npass && i + n < ops.size() &&
@@ -2855,9 +2924,14 @@ gol_status gol_step(gol_engine* e, uint64_t generations)
             GOL_TRY(wait_fresh_halos(e));
         } else {
             GOL_TRY(run_launch_op(e, op, xchg));
+            continue;
+        }
+        if (e->timing_every) {  // the round's launches start here
+            GOL_TRY(get_event(e, &rev.start));
+            HIP_TRY(hipEventRecord(rev.start, e->stream));
         }
     }
-    return GOL_OK;
+    return close_round();
 }
 
 gol_status gol_group_step(gol_engine** engines, int nranks, uint64_t generations)
@@ -3088,6 +3162,21 @@ gol_status gol_set_timing(gol_engine* e, int every)
     return GOL_OK;
 }
 
+// Copy a timing record into the caller's struct: all of it when the caller says it
+// has this header's layout (struct_size), else the r04 prefix only.
+static void put_timing(gol_timing* out, const gol_timing& t)
+{
+    if (out->struct_size == (uint32_t)sizeof(gol_timing)) {
+        *out = t;
+        out->struct_size = (uint32_t)sizeof(gol_timing);
+    } else {
+        static_assert(offsetof(gol_timing, struct_size) + sizeof(uint32_t) == GOL_TIMING_R04_BYTES,
+                      "r04 gol_timing prefix");
+        std::memcpy(out, &t, offsetof(gol_timing, struct_size));
+        out->struct_size = GOL_TIMING_R04_BYTES;
+    }
+}
+
 gol_status gol_get_timing(gol_engine* e, gol_timing* out)
 {
     if (!e || !out) return fail(GOL_EINVAL, "null argument");
@@ -3095,6 +3184,7 @@ gol_status gol_get_timing(gol_engine* e, gol_timing* out)
         gol_timing t{};
         for (auto* p : e->parts) {
             gol_timing pt{};
+            pt.struct_size = (uint32_t)sizeof(gol_timing);
             gol_status st = gol_get_timing(p, &pt);
             if (st != GOL_OK) return st;
             t.launches += pt.launches;
@@ -3105,15 +3195,19 @@ gol_status gol_get_timing(gol_engine* e, gol_timing* out)
             t.launch_rows += pt.launch_rows;
             t.exchanges += pt.exchanges;
             t.exchange_ms += pt.exchange_ms;
+            t.rounds += pt.rounds;
+            t.round_ms += pt.round_ms;
+            t.exchange_exposed_ms += pt.exchange_exposed_ms;
         }
         t.streams = (uint32_t)e->parts.size();
-        *out = t;
+        put_timing(out, t);
         return GOL_OK;
     }
     gol_status st = flush_timing(e);
     if (st != GOL_OK) return st;
-    *out = e->tm;
-    out->streams = 1;
+    gol_timing t = e->tm;
+    t.streams = 1;
+    put_timing(out, t);
     return GOL_OK;
 }
 

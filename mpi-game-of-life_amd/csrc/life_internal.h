@@ -131,10 +131,11 @@ constexpr bool handoff_kernel_exists(int K, RuleKind rule)
 
 // Multi-pass stencil kernels (StepArgs::npass > 1, life_stencil.h): 2-plane lane
 // groups at depths 12 and 16 (the generic-mask rule at 12 only, as its hand-off
-// kernels)
+// kernels).  Measured slower than single-pass launches (r05): the dev
+// build only (make dev), so the shipped library carries no multi-pass kernel.
 constexpr bool multipass_kernel_exists(int K, RuleKind rule, int planes)
 {
-    return planes == 2 && (K == 12 || (K == 16 && rule != RULE_GENERIC));
+    return kDevKernels && planes == 2 && (K == 12 || (K == 16 && rule != RULE_GENERIC));
 }
 
 // Steps per block of the stencil kernel's register prefetch ring (host copy of

@@ -224,20 +224,27 @@ static inline uint64_t last_word_mask(int64_t w)
     return rem ? ((1ULL << rem) - 1ULL) : ~0ULL;
 }
 
-/* Synthetic p=0.5 field: word (r,q) = splitmix64(seed, r*Wq+q), masked to w. */
-void oracle_bp_init_random(uint64_t* g, int64_t h, int64_t w, int64_t stride, uint64_t seed)
+/* Synthetic p=0.5 field: word (r,q) = splitmix64(seed, r*Wq+q), masked to w.
+ * _rows: field rows [row0, row0 + h) only (a rank's stripe of a larger field). */
+void oracle_bp_init_random_rows(uint64_t* g, int64_t row0, int64_t h, int64_t w, int64_t stride,
+                                uint64_t seed)
 {
     int64_t wq = (w + 63) / 64;
     for (int64_t r = 0; r < h; r++) {
         for (int64_t q = 0; q < stride; q++) {
             uint64_t v = 0;
             if (q < wq) {
-                v = splitmix64_at(seed, (uint64_t)r * (uint64_t)wq + (uint64_t)q);
+                v = splitmix64_at(seed, (uint64_t)(row0 + r) * (uint64_t)wq + (uint64_t)q);
                 if (q == wq - 1) v &= last_word_mask(w);
             }
             g[r * stride + q] = v;
         }
     }
+}
+
+void oracle_bp_init_random(uint64_t* g, int64_t h, int64_t w, int64_t stride, uint64_t seed)
+{
+    oracle_bp_init_random_rows(g, 0, h, w, stride, seed);
 }
 
 /* Order-independent digest: live count and sum over words of

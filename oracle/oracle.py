@@ -39,6 +39,7 @@ def _lib():
     lib.oracle_ref_baseline.argtypes = [i32, i32, i32, i32, u64, u32, u32]
     lib.oracle_ref_baseline.restype = i64
     lib.oracle_bp_init_random.argtypes = [vp, i64, i64, i64, u64]
+    lib.oracle_bp_init_random_rows.argtypes = [vp, i64, i64, i64, i64, u64]
     lib.oracle_bp_digest.argtypes = [vp, i64, i64, i64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.oracle_bp_pack_ascii.argtypes = [vp, ctypes.c_size_t, i64, i64, vp, i64]
     lib.oracle_bp_pack_ascii.restype = i32
@@ -90,6 +91,13 @@ def bp_random(h, w, seed=1, stride=None):
     stride = stride or words(w)
     g = np.zeros((h, stride), dtype=np.uint64)
     lib().oracle_bp_init_random(g.ctypes.data, h, w, stride, seed)
+    return g
+
+
+def bp_random_rows(row0, h, w, seed=1):
+    """Rows [row0, row0 + h) of bp_random(row0 + h, w, seed), without the rest."""
+    g = np.zeros((h, words(w)), dtype=np.uint64)
+    lib().oracle_bp_init_random_rows(g.ctypes.data, row0, h, w, words(w), seed)
     return g
 
 

@@ -142,6 +142,9 @@ def test_shipped_library_has_only_product_kernels(pkg):
     assert depths == {1, 2, 4, 6, 7, 8, 12, 16}
     assert {int(n) for _, _, n, _ in names} == {2}
     assert {(int(k), int(h)) for k, _, _, h in names if int(h)} == {(k, 1) for k in (4, 6, 7, 8, 12, 16)}
+    # (r06) no multi-pass instantiation (template flag MP = true): dev build only
+    full = set(re.findall(rb"life_tb_kernelILi(\d+)ELi(\d)ELi(\d)ELb(\d)ELi(\d)ELb(\d)E", blob))
+    assert full and {mp for *_, mp in full} == {b"0"}
     # the resident kernel: 5 rows-per-wavefront variants x 3 rule kinds
     res = set(re.findall(rb"life_res_kernelILi(\d)ELi(\d)E", blob))
     assert res == {(str(m).encode(), str(r).encode()) for m in (2, 3, 4, 6, 8) for r in range(3)}

@@ -107,3 +107,42 @@ def test_c5_full_field_one_gpu_vs_oracle(pkg, oracle, rule):
         got = e.digest()
     g = oracle.bp_run(oracle.bp_random(n, n, 1), n, 16, R, threads=THREADS)
     assert got == oracle.bp_digest(g, n)
+
+
+def test_c3_headline_1000_generations_vs_oracle_fixed_point(pkg, oracle):
+    """The headline job itself (65536^2, seed 1, B/S2, 1000 generations through
+    the default engine: 62 age-skewed K = 16 launches + a depth-8 one, graph
+    replay) against the oracle.  B/S2 has no births (Parallel_Life_MPI.cpp:44-50),
+    so the live set only shrinks and reaches a fixed point: the oracle iterates
+    until bp_run(g, 1) == g (about ten generations), which is then its state at
+    every later generation, 1000 included."""
+    with pkg.Engine(N, N, device=0) as e:
+        assert e.tb_depth == 16 and e.resident is None
+        e.init_random(1)
+        e.step(1000)
+        got = e.digest()
+    g = oracle.bp_random(N, N, 1)
+    for gen in range(1, 201):
+        nxt = oracle.bp_run(g, N, 1, oracle.REF_RULE, threads=THREADS)
+        if (nxt == g).all():
+            break
+        g = nxt
+    else:
+        pytest.fail("the oracle's B/S2 field reached no fixed point in 200 generations")
+    assert gen < 1000
+    assert got == oracle.bp_digest(g, N), f"fixed point reached at generation {gen}"
+
+
+def test_conway_16384_1000_generations_vs_oracle(pkg, oracle):
+    """B3/S23 for 1000 generations at the largest size the oracle evolves in well
+    under a minute on the box (16384^2: 2.7e11 cell-generations), through the
+    default engine there (K = 16 streaming launches of the skewed plan), against
+    the oracle's own 1000 generations."""
+    n = 16384
+    with pkg.Engine(n, n, rule=pkg.CONWAY, device=0) as e:
+        assert e.tb_depth == 16 and e.resident is None, (e.tb_depth, e.resident)
+        e.init_random(3)
+        e.step(1000)
+        got = e.digest()
+    g = oracle.bp_run(oracle.bp_random(n, n, 3), n, 1000, oracle.CONWAY, threads=THREADS)
+    assert got == oracle.bp_digest(g, n)

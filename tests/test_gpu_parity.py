@@ -306,18 +306,55 @@ def test_c2_4096_per_generation(pkg, oracle, rule, kernel):
         assert (e.store_packed() == want[16]).all()
 
 
-def test_c2_4096_1000_generations_depths_agree(pkg):
-    """Size-independent property: every fused depth, both block closures, gives
-    the same field after 1000 Conway generations."""
-    digests = set()
+_C2_1000 = {}
+
+
+def c2_oracle_1000(oracle, rule):
+    """The oracle's 4096^2 field (seed 1) after 1000 generations (digest), once per
+    rule per session (~2-5 s on 16 threads)."""
+    if rule not in _C2_1000:
+        R = rules(oracle)[rule]
+        g = oracle.bp_run(oracle.bp_random(4096, 4096, 1), 4096, 1000, R, threads=16)
+        _C2_1000[rule] = oracle.bp_digest(g, 4096)
+    return _C2_1000[rule]
+
+
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+@pytest.mark.parametrize("kernel", ["resident", "streaming"])
+def test_c2_4096_1000_generations_vs_oracle(pkg, oracle, rule, kernel):
+    """C2 as BASELINE.json states it (4096^2, p = 0.5, 1000 generations, one
+    MI355X): the default engine (the resident kernel, ONE launch for the 1000
+    generations) and the K = 16 streaming engine (62 full-depth launches + a
+    depth-8 one) against the oracle's 1000 generations, both rules (r06; until
+    r05 this was "every depth gives the same digest", GPU against GPU).
+    Parallel_Life_MPI.cpp:37-54 per generation, :215-221 the loop."""
+    R = rules(oracle)[rule]
+    want = c2_oracle_1000(oracle, rule)
+    kw = {} if kernel == "resident" else {"resident": 1, "tb_depth": 16}
+    with pkg.Engine(4096, 4096, rule=R, device=0, **kw) as e:
+        assert (e.resident is not None) == (kernel == "resident")
+        if kernel == "streaming":
+            assert e.tb_depth == 16
+        e.init_random(1)
+        e.step(1000)
+        assert e.digest() == want
+        if rule == "conway":  # still active: the check is not a fixed point's
+            e.step(1)
+            assert e.digest() != want
+
+
+def test_c2_4096_1000_generations_every_depth_vs_oracle(pkg, oracle):
+    """Every fused depth and both block closures after 1000 Conway generations
+    (one gol_step call: a depth-d kernel and the remainder depths) against the
+    oracle."""
+    want = c2_oracle_1000(oracle, "conway")
     for depth in DEPTHS:
         for handoff in ((1, 2) if depth >= 4 else (1,)):
-            with pkg.Engine(4096, 4096, rule=(1 << 3, 12), device=0, tb_depth=depth,
+            with pkg.Engine(4096, 4096, rule=pkg.CONWAY, device=0, tb_depth=depth,
                             handoff=handoff) as e:
                 e.init_random(1)
                 e.step(1000)
-                digests.add(e.digest())
-    assert len(digests) == 1
+                assert e.digest() == want, (depth, handoff)
 
 
 # ------------------------------------------------------------ timing API
@@ -331,6 +368,29 @@ def test_timing_counters(pkg):
     assert t["launches"] == 3
     assert t["kernel_ms"] > 0
     assert t["cell_gens"] == 1024 * 1024 * 20
+
+
+def test_timing_struct_size(pkg):
+    """gol_get_timing never writes past a caller's older gol_timing: without this
+    header's struct_size it writes the r04 fields (40 bytes) only."""
+    import ctypes
+    with pkg.Engine(512, 512, device=0, tb_depth=8) as e:
+        e.init_random(1)
+        e.set_timing(1)
+        e.step(16)
+        e.sync()
+        full = ctypes.sizeof(pkg.Timing)
+        buf = (ctypes.c_uint8 * (full + 16))(*([0xAB] * (full + 16)))
+        struct_size = ctypes.c_uint32.from_buffer(buf, 36)
+        struct_size.value = 40  # an r04 caller's (garbage) value
+        assert pkg.lib().gol_get_timing(e._h, ctypes.cast(buf, ctypes.POINTER(pkg.Timing))) == 0
+        assert struct_size.value == 40
+        assert bytes(buf[40:]) == bytes([0xAB] * (full + 16 - 40))
+        assert ctypes.c_uint64.from_buffer(buf, 0).value == 2  # launches
+        struct_size.value = full
+        assert pkg.lib().gol_get_timing(e._h, ctypes.cast(buf, ctypes.POINTER(pkg.Timing))) == 0
+        assert struct_size.value == full
+        assert bytes(buf[full:]) == bytes([0xAB] * 16)
 
 
 def test_timing_sampled(pkg):

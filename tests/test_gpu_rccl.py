@@ -116,6 +116,70 @@ def test_rccl_self_loop_c4_rank_shape(pkg, monkeypatch):
     assert (out[0][1] == out[1][1]).all()
 
 
+@pytest.mark.parametrize("overlap", [1, 2])
+def test_rccl_self_loop_c5_rank_shape(pkg, oracle, monkeypatch, overlap):
+    """The C5 per-rank shape (rank 3 of 8 of 262144^2: 32768 own rows x 262144
+    columns + 2 x Hx halo rows, default K = 16 and Hx = 12K = 192, 6 MiB messages)
+    through RCCL every round, both exchange modes: one partial round (16
+    generations) against the oracle evolving the mirrored extended stripe
+    (Parallel_Life_MPI.cpp:37-54 on :70-81's stripe, with the halo rows the
+    exchange :104-145 is meant to deliver), then two full rounds and a partial one
+    bytewise against the same engine over the host loopback transport."""
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    n, world, rank = 262144, 8, 3
+    chunks = [16, 2 * 192 + 40]
+    out = []
+    for mode in ("rccl", "host"):
+        kw = dict(uid=pkg.unique_id()) if mode == "rccl" else dict(transport=lambda su, sd: (su, sd))
+        with pkg.Engine(n, n, rule=pkg.CONWAY, device=0, rank=rank, nranks=world,
+                        exchange_overlap=overlap, **kw) as e:
+            assert (e.rows, e.tb_depth, e.halo_depth) == (32768, 16, 192)
+            e.init_random(5)
+            res = []
+            for c in chunks:
+                e.step(c)
+                res.append((e.digest(), e.store_packed()))
+            row0 = e.row0
+        out.append(res)
+    for i, ((da, a), (db, b)) in enumerate(zip(*out)):
+        assert da == db and (a == b).all(), f"RCCL vs host loopback, chunk {i}"
+    # the first chunk against the oracle's mirrored stripe (the field's rows of
+    # this rank, splitmix64 seed 5)
+    own = oracle.bp_random_rows(row0, 32768, n, 5)
+    want = mirrored_round(oracle, own, n, 16, oracle.CONWAY, 192, True, True)
+    assert (out[0][0][1] == want).all()
+    assert out[0][0][0][0] == int(np.unpackbits(want.view(np.uint8)).sum())
+
+
+@pytest.mark.parametrize("overlap", [1, 2])
+def test_rank_timing_spans_add_up(pkg, monkeypatch, overlap):
+    """gol_timing's round spans (r06, bench.py rank_breakdown): per halo round
+    one compute-stream span, the exchange split into its exposed and hidden
+    parts; spans + exposed exchange fit in the wall time of the steps, both
+    exchange modes."""
+    import time
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    with pkg.Engine(16384, 16384, rule=pkg.CONWAY, device=0, rank=1, nranks=4,
+                    uid=pkg.unique_id(), exchange_overlap=overlap) as e:
+        hx = e.halo_depth
+        e.init_random(1)
+        e.step(4 * hx)
+        e.sync()
+        e.set_timing(8)
+        e.reset_timing()
+        t0 = time.perf_counter()
+        e.step(4 * hx)
+        e.sync()
+        wall = (time.perf_counter() - t0) * 1e3
+        t = e.timing()
+    assert t["rounds"] == 4 and t["exchanges"] == 4, t
+    assert t["round_ms"] > 0 and t["exchange_ms"] > 0
+    assert 0 <= t["exchange_exposed_ms"] <= t["exchange_ms"] + 1e-6
+    if overlap == 1:  # blocking: every exchange sits between two rounds
+        assert t["exchange_exposed_ms"] == pytest.approx(t["exchange_ms"])
+    assert t["round_ms"] + t["exchange_exposed_ms"] <= wall * 1.01 + 0.05, (t, wall)
+
+
 def test_rccl_self_loop_two_communicators(pkg, monkeypatch):
     """A second engine on another self-loop communicator in the same process, and
     destroy/re-create: communicators are per engine."""
