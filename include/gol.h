@@ -211,6 +211,15 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0,
 gol_status gol_plan_info(gol_engine* e, uint32_t* strip_lanes, uint32_t* rows_per_wave,
                          uint32_t* word_planes);
 
+/* (r06) Resident plan details: rows per wavefront, band rows per tile, epoch
+ * length K (generations between the tiles' swaps through memory), and
+ * *swap_every: the generations between the wavefronts' row swaps through LDS
+ * inside a tile (1 = every generation, life_res_kernel; >= 2 = the wave-level
+ * temporal blocking of life_resident_mb.hip).  All 0 when the engine does not run
+ * the resident kernel.  Out pointers may be NULL. */
+gol_status gol_plan_resident_rows(gol_engine* e, uint32_t* rows, uint32_t* band_rows,
+                                  uint32_t* epoch, uint32_t* swap_every);
+
 /* Whether full-depth launches use hand-off row blocks (gol_config.handoff, as
  * the planner resolved it): 1 = yes, 0 = every block recomputes its halo. */
 gol_status gol_plan_handoff(gol_engine* e, uint32_t* handoff);

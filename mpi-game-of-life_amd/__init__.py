@@ -36,6 +36,7 @@ EXPORTS = [
     "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
     "gol_plan_resident", "gol_plan_skew", "gol_plan_columns", "gol_plan_tuning",
     "gol_digest_rows", "gol_comm_info", "gol_plan_model", "gol_plan_passes",
+    "gol_plan_resident_rows",
 ]
 
 # gol_plan_tuning's variants (engine.cpp kTuneVariantNames): 0 = the models' plan
@@ -183,6 +184,7 @@ def lib():
     pf32 = ctypes.POINTER(ctypes.c_float)
     L.gol_plan_tuning.argtypes = [vp, ctypes.POINTER(u32), pf32, pf32]
     L.gol_plan_passes.argtypes = [vp, ctypes.POINTER(u32)]
+    L.gol_plan_resident_rows.argtypes = [vp] + [ctypes.POINTER(u32)] * 4
     L.gol_digest_rows.argtypes = [vp, u64, u64, pu64, pu64]
     pi32 = ctypes.POINTER(ctypes.c_int)
     L.gol_comm_info.argtypes = [vp, pi32, pi32, pi32, pi32, pi32]
@@ -198,7 +200,8 @@ def lib():
                  "gol_create_group", "gol_group_step", "gol_plan_info", "gol_plan_handoff",
                  "gol_plan_resident", "gol_plan_skew", "gol_plan_columns",
                  "gol_create_rank_transport", "gol_round_schedule", "gol_plan_tuning",
-                 "gol_digest_rows", "gol_comm_info", "gol_plan_model", "gol_plan_passes"]:
+                 "gol_digest_rows", "gol_comm_info", "gol_plan_model", "gol_plan_passes",
+                 "gol_plan_resident_rows"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -322,6 +325,11 @@ class Engine:
         _check(lib().gol_plan_resident(self._h, ctypes.byref(on), ctypes.byref(nb), ctypes.byref(ns)))
         # resident kernel: (bands, strips) of its tiles, or None
         self.resident = (nb.value, ns.value) if on.value else None
+        rr = [ctypes.c_uint32() for _ in range(4)]
+        _check(lib().gol_plan_resident_rows(self._h, *(ctypes.byref(v) for v in rr)))
+        # resident kernel: rows per wavefront, band rows, epoch K, generations
+        # between the wavefronts' LDS row swaps (1: every one), or None
+        self.resident_rows = tuple(v.value for v in rr) if on.value else None
         ro, ry, uo = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
         _check(lib().gol_plan_skew(self._h, ctypes.byref(ro), ctypes.byref(ry), ctypes.byref(uo)))
         # age-skewed row blocks: (rows_old, rows_young, units_old), or None

@@ -298,6 +298,9 @@ struct gol_engine {
         // 609-614 us per 1000 generations, profiles/r03/ab_resident_coop.jsonl);
         // the planner's occupancy check and the bounded waits cover it by default
         bool coop = false;
+        // wave-level temporal blocking (life_resident_mb.hip): wavefronts swap rows
+        // through LDS every `mb` generations; 1 = every generation (life_res_kernel)
+        int mb = 1;
         hipEvent_t ev_in = nullptr, ev_out = nullptr;  // ordering with the shared stream
     } res;
 
@@ -1646,6 +1649,12 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
         const char* v = std::getenv("GOL_DEV_RES_COOP");
         e->res.coop = v && std::atoi(v) == 1;
     }
+    if (const char* v = std::getenv("GOL_DEV_RES_MB")) {  // dev A/B of the blocking depth
+        const int mb = std::atoi(v);
+        if (mb >= 2 && gol::resident_mb_exists(e->res.rows, mb, e->rule) &&
+            gol::resident_mb_blocks_per_cu(e->res.rows, mb, e->rule) >= 1)
+            e->res.mb = mb;
+    }
     e->K = (uint32_t)e->res.K;
     return GOL_OK;
 }
@@ -1702,9 +1711,14 @@ gol_status step_resident(gol_engine* e, uint64_t generations)
 #endif
         hipEvent_t e0, e1;
         GOL_TRY(timing_begin(e, rs, &e0, &e1));
-        HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, rs, r.coop));
-        // lanes process every held row of every tile, every generation
-        const double comp = (double)g * r.bands * r.strips * gol::kResWaves * r.rows * 64.0 * 64.0;
+        if (r.mb > 1)
+            HIP_TRY(gol::launch_resident_mb(a, r.rows, r.mb, e->rule, r.bands * r.strips, rs));
+        else
+            HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, rs, r.coop));
+        // lanes process every held row of every tile, every generation (wave-level
+        // blocking: rows + mb - 1 per generation on average over a super-step)
+        const double comp = (double)g * r.bands * r.strips * gol::kResWaves * (r.rows + r.mb - 1) *
+                            64.0 * 64.0;
         GOL_TRY(timing_end(e, rs, e0, e1, (double)e->H * (double)e->W * g, comp));
         const uint32_t epochs = (uint32_t)((g + r.K - 1) / r.K);
         r.flag_base += epochs;
@@ -3308,6 +3322,18 @@ gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint3
     *on = e->res.on ? 1u : 0u;
     if (bands) *bands = (uint32_t)e->res.bands;
     if (strips) *strips = (uint32_t)e->res.strips;
+    return GOL_OK;
+}
+
+gol_status gol_plan_resident_rows(gol_engine* e, uint32_t* rows, uint32_t* band_rows,
+                                  uint32_t* epoch, uint32_t* swap_every)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    const bool on = e->parts.empty() && e->res.on;
+    if (rows) *rows = on ? (uint32_t)e->res.rows : 0u;
+    if (band_rows) *band_rows = on ? (uint32_t)e->res.band_rows : 0u;
+    if (epoch) *epoch = on ? (uint32_t)e->res.K : 0u;
+    if (swap_every) *swap_every = on ? (uint32_t)e->res.mb : 0u;
     return GOL_OK;
 }
 

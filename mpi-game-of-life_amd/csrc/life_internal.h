@@ -216,6 +216,16 @@ struct ResArgs {
 hipError_t launch_resident(const ResArgs& a, int rows, RuleKind rule, int grid, hipStream_t s,
                            bool coop = false);
 int resident_blocks_per_cu(int rows, RuleKind rule);
+// The resident kernel with wave-level temporal blocking (life_resident_mb.hip, r06):
+// wavefronts swap MB rows through LDS every MB generations.  (rows, mb) pairs:
+// (the generic-mask rule at rows = mb = 4 spills: not offered)
+constexpr bool resident_mb_exists(int rows, int mb, RuleKind rule)
+{
+    return mb >= 2 && mb <= rows && rows <= 4 && !(rule == RULE_GENERIC && mb == 4);
+}
+hipError_t launch_resident_mb(const ResArgs& a, int rows, int mb, RuleKind rule, int grid,
+                              hipStream_t s);
+int resident_mb_blocks_per_cu(int rows, int mb, RuleKind rule);
 
 // Device-side synthetic init: buffer rows [row_base, row_base+nrows) get field
 // rows [glob_row0, glob_row0+nrows).
