@@ -177,3 +177,64 @@ def test_resident_cooperative_launch(pkg, oracle, monkeypatch, rule):
         e.step(40)
         got = e.store_packed()
     assert (got == oracle.bp_run(g, w, 77, R)).all()
+
+
+# ------------------------------------------------ wave-level temporal blocking
+# life_resident_mb.hip (r06): the wavefronts of a tile swap MB rows through LDS
+# every MB generations.  GOL_DEV_RES_MB selects it at create (the planner's
+# default is reported by Engine.resident_rows[3]).
+MB_CASES = [(2, 2), (3, 2), (3, 3), (4, 2), (4, 3), (4, 4)]
+
+
+@pytest.mark.parametrize("rows,mb", MB_CASES, ids=lambda v: str(v))
+@pytest.mark.parametrize("rule", ["ref", "conway", "highlife", "b0"])
+def test_resident_mb_random_fields(pkg, oracle, monkeypatch, rows, mb, rule):
+    """Every (rows, MB) kernel vs the oracle: one strip and multi-strip rows
+    (halo lanes), partial last bands, epoch lengths K that are and are not
+    multiples of MB (partial last super-steps), generation counts that end
+    inside a super-step and inside an epoch."""
+    if rule == "highlife" and mb == 4:
+        pytest.skip("no generic-mask kernel at MB = 4 (it spills)")
+    monkeypatch.setenv("GOL_DEV_RES_MB", str(mb))
+    R = rules(oracle)[rule]
+    for h, w, K in ((17, 129, 3), (100, 3969, 7), (64, 4097, 8), (257, 200, 5),
+                    (1000, 1000, 16), (130, 8000, 11)):
+        seed = 3 * h + w + mb
+        g = oracle.bp_random(h, w, seed)
+        try:
+            e = pkg.Engine(h, w, rule=R, device=0, resident=2, rows_per_wave=rows, tb_depth=K)
+        except pkg.GolError:
+            continue  # (rows, K) does not fit the shape
+        with e:
+            assert e.resident_rows == (rows, e.resident_rows[1], K, mb), e.resident_rows
+            for n in (1, mb, K + 1, 2 * K + mb - 1, 45):
+                e.load_packed(g)
+                e.step(n)
+                ref = oracle.bp_run(g, w, n, R)
+                assert (e.store_packed() == ref).all(), f"{h}x{w} K {K} gens {n}"
+
+
+@pytest.mark.parametrize("mb", [2, 3])
+@pytest.mark.parametrize("rule", ["ref", "conway"])
+def test_resident_mb_c2_auto_plan(pkg, oracle, monkeypatch, mb, rule):
+    """The C2 field with the auto resident plan (4096^2: 256 tiles of 16 rows,
+    K = 16) and wave-level blocking, per generation for the early B/S2
+    generations, and 1000 generations against the oracle."""
+    monkeypatch.setenv("GOL_DEV_RES_MB", str(mb))
+    R = rules(oracle)[rule]
+    n = 4096
+    g0 = oracle.bp_random(n, n, 1)
+    want = {0: g0}
+    for gen in range(1, 10):
+        want[gen] = oracle.bp_run(want[gen - 1], n, 1, R, threads=16)
+    with pkg.Engine(n, n, rule=R, device=0) as e:
+        assert e.resident is not None
+        rows = e.resident_rows[0]
+        assert e.resident_rows[3] == (mb if mb <= rows else 1), e.resident_rows
+        for gens in range(1, 10):
+            e.init_random(1)
+            e.step(gens)
+            assert e.digest() == oracle.bp_digest(want[gens], n), gens
+        e.init_random(1)
+        e.step(1000)
+        assert e.digest() == oracle.bp_digest(oracle.bp_run(g0, n, 1000, R, threads=16), n)
