@@ -257,7 +257,9 @@ gol_status gol_plan_tuning(gol_engine* e, uint32_t* variant, float* tuned_us, fl
 
 /* Passes per full-depth launch of the first full-depth plan: 1, or 2-3 for
  * multi-pass launches (each launch runs that many depth-K passes over its row
- * blocks, alternating direction; dev switch GOL_DEV_PASSES at create). */
+ * blocks, alternating direction; dev switch GOL_DEV_PASSES at create, read only by
+ * the dev build, libgol_dev.so: the shipped library has no multi-pass kernel
+ * since r06 and always reports 1). */
 gol_status gol_plan_passes(gol_engine* e, uint32_t* passes);
 
 /* gol_digest restricted to field rows [row0, row0 + rows) (for a rank engine:
@@ -362,7 +364,13 @@ typedef struct gol_plan_summary {
     int64_t blocks;                 /* row blocks per strip (summed over segments) */
     int32_t handoff, tail_off;      /* hand-off blocks, their kernel's tail offset (-1) */
     uint32_t candidates;            /* autotuner variants built for this plan */
-    uint32_t passes;                /* passes per full-depth launch (gol_plan_passes) */
+    uint32_t passes;                /* passes per full-depth launch (gol_plan_passes);
+                                       always 1 with the shipped library (multi-pass
+                                       kernels: dev build).  The model assumes the
+                                       multi-pass kernels fit the same occupancies
+                                       as the single-pass ones (their real occupancy
+                                       may be lower, where the engine would then
+                                       fall back to single-pass launches). */
 } gol_plan_summary;
 gol_status gol_plan_model(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
                           int cus, int occ_classic, int occ_hand, gol_plan_summary* out);

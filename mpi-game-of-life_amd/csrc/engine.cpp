@@ -1649,12 +1649,16 @@ gol_status plan_resident(gol_engine* e, const gol_config* cfg)
         const char* v = std::getenv("GOL_DEV_RES_COOP");
         e->res.coop = v && std::atoi(v) == 1;
     }
-    if (const char* v = std::getenv("GOL_DEV_RES_MB")) {  // dev A/B of the blocking depth
+#if GOL_DEV_KERNELS
+    // dev build: the wave-level temporal blocking of life_resident_mb.hip (r06,
+    // measured slower at every MB: DESIGN §4)
+    if (const char* v = std::getenv("GOL_DEV_RES_MB")) {
         const int mb = std::atoi(v);
         if (mb >= 2 && gol::resident_mb_exists(e->res.rows, mb, e->rule) &&
             gol::resident_mb_blocks_per_cu(e->res.rows, mb, e->rule) >= 1)
             e->res.mb = mb;
     }
+#endif
     e->K = (uint32_t)e->res.K;
     return GOL_OK;
 }
@@ -1711,9 +1715,11 @@ gol_status step_resident(gol_engine* e, uint64_t generations)
 #endif
         hipEvent_t e0, e1;
         GOL_TRY(timing_begin(e, rs, &e0, &e1));
+#if GOL_DEV_KERNELS
         if (r.mb > 1)
             HIP_TRY(gol::launch_resident_mb(a, r.rows, r.mb, e->rule, r.bands * r.strips, rs));
         else
+#endif
             HIP_TRY(gol::launch_resident(a, r.rows, e->rule, r.bands * r.strips, rs, r.coop));
         // lanes process every held row of every tile, every generation (wave-level
         // blocking: rows + mb - 1 per generation on average over a super-step)

@@ -216,8 +216,9 @@ struct ResArgs {
 hipError_t launch_resident(const ResArgs& a, int rows, RuleKind rule, int grid, hipStream_t s,
                            bool coop = false);
 int resident_blocks_per_cu(int rows, RuleKind rule);
-// The resident kernel with wave-level temporal blocking (life_resident_mb.hip, r06):
-// wavefronts swap MB rows through LDS every MB generations.  (rows, mb) pairs:
+// The resident kernel with wave-level temporal blocking (life_resident_mb.hip, r06,
+// dev build only: slower than life_res_kernel at every MB): wavefronts
+// swap MB rows through LDS every MB generations.  (rows, mb) pairs:
 // (the generic-mask rule at rows = mb = 4 spills: not offered)
 constexpr bool resident_mb_exists(int rows, int mb, RuleKind rule)
 {

@@ -186,9 +186,17 @@ def test_resident_cooperative_launch(pkg, oracle, monkeypatch, rule):
 MB_CASES = [(2, 2), (3, 2), (3, 3), (4, 2), (4, 3), (4, 4)]
 
 
+@pytest.fixture
+def mb_kernels(pkg):
+    """The MB kernels are in the dev build only (measured slower):
+    these tests run with GOL_LIB=.../libgol_dev.so and skip otherwise."""
+    if b"life_res_mb_kernel" not in open(pkg.LIB_PATH, "rb").read():
+        pytest.skip("wave-level blocking kernels are in the dev build only (GOL_LIB=libgol_dev.so)")
+
+
 @pytest.mark.parametrize("rows,mb", MB_CASES, ids=lambda v: str(v))
 @pytest.mark.parametrize("rule", ["ref", "conway", "highlife", "b0"])
-def test_resident_mb_random_fields(pkg, oracle, monkeypatch, rows, mb, rule):
+def test_resident_mb_random_fields(pkg, oracle, monkeypatch, mb_kernels, rows, mb, rule):
     """Every (rows, MB) kernel vs the oracle: one strip and multi-strip rows
     (halo lanes), partial last bands, epoch lengths K that are and are not
     multiples of MB (partial last super-steps), generation counts that end
@@ -216,7 +224,7 @@ def test_resident_mb_random_fields(pkg, oracle, monkeypatch, rows, mb, rule):
 
 @pytest.mark.parametrize("mb", [2, 3])
 @pytest.mark.parametrize("rule", ["ref", "conway"])
-def test_resident_mb_c2_auto_plan(pkg, oracle, monkeypatch, mb, rule):
+def test_resident_mb_c2_auto_plan(pkg, oracle, monkeypatch, mb_kernels, mb, rule):
     """The C2 field with the auto resident plan (4096^2: 256 tiles of 16 rows,
     K = 16) and wave-level blocking, per generation for the early B/S2
     generations, and 1000 generations against the oracle."""
