@@ -129,7 +129,7 @@ def counters_for(cfg):
     skew variants move it by ~3%; at the same work ratio the counters move by well
     under 1%)."""
     recs = []
-    for rnd in ("r05", "r04", "r03", "r02"):  # newest first
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):  # newest first
         recs += (load_json(f"profiles/{rnd}/counters.json") or {}).get("records", [])
     keys = ("size", "rule", "tb_depth", "streams", "n_gpus", "handoff")
     best = None
