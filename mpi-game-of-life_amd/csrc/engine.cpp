@@ -232,6 +232,7 @@ struct gol_engine {
     int cur = 0;
     int nbuf = 2;
     uint32_t npass = 1;       // passes per full-depth launch the engine may run
+    uint32_t xcd_shift = 0;   // (r06 dev A/B) StepArgs::xcd_shift, GOL_DEV_XCD_SHIFT
     uint32_t shadow_off = 0;  // bytes from a buffer word to its shadow
     uint32_t* mpflags = nullptr;  // multi-pass head/done flags: 4 x max units
 
@@ -1431,6 +1432,15 @@ gol_status init_common(gol_engine* e, uint64_t h, uint64_t w, const gol_config* 
 
     const size_t words = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
     decide_passes(e, words);
+    // (r06 dev A/B) GOL_DEV_XCD_SHIFT = "c0c1...c7:m": speed class 0-3 of the
+    // workgroups with blockIdx mod 8 == x, and the strip modulus m (life_stencil.h)
+    if (const char* v = gol::kDevKernels ? std::getenv("GOL_DEV_XCD_SHIFT") : nullptr) {
+        uint32_t code = 0;
+        int i = 0;
+        for (; i < 8 && v[i] >= '0' && v[i] <= '3'; ++i) code |= (uint32_t)(v[i] - '0') << (2 * i);
+        const int m = (i == 8 && v[8] == ':') ? std::atoi(v + 9) : 0;
+        if (m >= 1 && m <= 255) e->xcd_shift = code | ((uint32_t)m << 16);
+    }
     const size_t halves = e->npass > 1 ? 2 : 1;
     e->nbuf = e->npass > 1 ? 4 : 2;
     e->shadow_off = e->npass > 1 ? (uint32_t)(words * sizeof(uint64_t)) : 0u;
@@ -1809,6 +1819,13 @@ gol_status launch(gol_engine* e, int plan, uint32_t depth, bool swap = true,
         a.rows_per_wave = p.rows_young;
         a.rows_old = p.rows_old;
         a.units_old = p.units_old;
+    }
+    // (r06 dev A/B, GOL_DEV_XCD_SHIFT) per-XCD row shift between paired blocks:
+    // blocks keep >= the length their closure needs after giving up 8 rows
+    if (e->xcd_shift && p.segs.size() == 1) {
+        const int64_t shortest = p.rows_old ? std::min<int64_t>(p.rows_old, p.rows_young) : p.rpw;
+        const bool fits = hand ? handoff_fits(shortest - 8, (int)depth, e->planes) : shortest - 8 >= 2;
+        if (fits) a.xcd_shift = e->xcd_shift;
     }
     a.edge = p.edge;
     a.right_q0 = p.right_q0;

@@ -107,6 +107,10 @@ struct StepArgs {
     int64_t half_q0, half_hi;
     int64_t pair0, pair_units;
     const int64_t* pairs;
+    // (r06 dev A/B) per-XCD row shift between paired blocks (life_stencil.h):
+    // bits 2x..2x+1 = speed class of blockIdx mod 8 == x, bits 16-23 = strip
+    // modulus m; 0 = off
+    uint32_t xcd_shift;
 };
 
 // Fused depths with an instantiated kernel, largest first.  The shipped library

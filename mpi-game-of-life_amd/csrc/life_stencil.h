@@ -689,6 +689,37 @@ void life_tb_kernel(StepArgs a)
         }
         planned_end = sg.out_lo + ny * a.rows_per_wave + jo * a.rows_old;
     }
+    // (r06 dev A/B, GOL_DEV_XCD_SHIFT, dev build only; measured 7% slower at the
+    // 8-way rank shape whatever the table) Per-XCD row shift: inside a strip,
+    // blocks pair up from the top as (1, 2), (3, 4), ... (never the first or the
+    // last block), and in the pairs of every m-th strip the block whose wavefront's
+    // workgroup lands on the faster XCD class (blockIdx mod 8 under round-robin
+    // dispatch; codes in 2-bit fields, higher = faster) takes 8 rows from its
+    // partner.  A pair's rows stay its rows, so every strip is still tiled exactly
+    // whatever XCD the workgroups really land on; 8 rows keep the hand-off
+    // tail-offset class and the even block starts.
+#if GOL_DEV_KERNELS
+    if (a.xcd_shift && !pu) {
+        const uint32_t m = (a.xcd_shift >> 16) & 0xffu;
+        const int32_t j = (int32_t)blk, nb = (int32_t)sg.nblk;
+        const int32_t jp = (j & 1) ? j : j - 1;  // the pair's upper block
+        if (m && jp >= 1 && jp + 1 <= nb - 2 && (uint32_t)u_strip % m == 0) {
+            auto code_of = [&](int32_t jj) {
+                const uint32_t uu = (uint32_t)sg.unit0 + (uint32_t)(nb - 1 - jj) * (uint32_t)a.strips +
+                                    (uint32_t)u_strip;
+                return (a.xcd_shift >> (2 * ((uu / kWavesPerBlock) & 7u))) & 3u;
+            };
+            const uint32_t cu = code_of(jp), cl = code_of(jp + 1);
+            const int32_t d = cu > cl ? 8 : (cu < cl ? -8 : 0);  // rows the upper block gains
+            if (j == jp) {
+                rlen += d;
+            } else {
+                rb += d;
+                rlen -= d;
+            }
+        }
+    }
+#endif
     const int64_t re = min(rb + rlen, sg.out_hi);
     // step counts and indices are 32-bit (a block has at most rows_per_wave + 2K
     // steps): uniform 32-bit compares stay on the scalar unit, 64-bit ones do not

@@ -106,3 +106,24 @@ def test_skew_shapes_vs_oracle(pkg, oracle, h, w, skewed, rule):
         got = e.digest()
     g = oracle.bp_run(oracle.bp_random(h, w, 11), w, gens, R, threads=THREADS)
     assert got == oracle.bp_digest(g, w)
+
+
+@pytest.mark.parametrize("shift", ["11310011:1", "33000000:1", "01230123:2", "30303030:1"])
+@pytest.mark.parametrize("handoff", [1, 2])
+def test_xcd_row_shift_vs_oracle(pkg, oracle, monkeypatch, shift, handoff):
+    """(r06 dev A/B, GOL_DEV_XCD_SHIFT, dev build; green on the shipped-library build
+    that carried it, profiles/r06/gpu_tests_xcd_shift.log) paired blocks of a strip trade 8 rows by
+    the speed class of their workgroups' XCD: every strip stays tiled exactly, with
+    hand-off and classic blocks, the skewed lengths and the launch's remainder
+    depths.  B3/S23 so births cross the moved block seams."""
+    if b"life_res_mb_kernel" not in open(pkg.LIB_PATH, "rb").read():
+        pytest.skip("the row shift is in the dev build only (GOL_LIB=.../libgol_dev.so)")
+    monkeypatch.setenv("GOL_DEV_XCD_SHIFT", shift)
+    rows, gens = 8448, 16 + 8 + 5
+    with pkg.Engine(rows, W, rule=pkg.CONWAY, device=0, handoff=handoff, streams=1) as e:
+        assert e.age_skew is not None
+        e.init_random(5)
+        e.step(gens)
+        got = e.digest()
+    g = oracle.bp_run(oracle.bp_random(rows, W, 5), W, gens, oracle.CONWAY, threads=THREADS)
+    assert got == oracle.bp_digest(g, W)

@@ -89,6 +89,9 @@ def main():
                    "full-depth launch (1 = single-pass launches, 2-3 multi-pass)")
     p.add_argument("--shrinks", default="0", help="GOL_DEV_RANK_SHRINK values: 0 = one region "
                    "for the full-depth launches of a round (default), 1 = shrinking regions")
+    p.add_argument("--env-var", default="", help="another create-time switch to A/B "
+                   "(e.g. GOL_DEV_XCD_SHIFT)")
+    p.add_argument("--env-values", default="", help="its values, ';'-separated (auto = unset)")
     a = p.parse_args()
     if a.lib:
         os.environ["GOL_LIB"] = os.path.abspath(a.lib)
@@ -110,11 +113,19 @@ def main():
                                     os.environ.pop("GOL_DEV_AGE_SKEW", None)
                                 else:
                                     os.environ["GOL_DEV_AGE_SKEW"] = sk
-                                e = rank_engine(pkg, n, rank, N, tp, a.handoff, ov, trn, hx)
-                                e.init_random(1)
-                                e.step(a.gens)
-                                e.sync()
-                                engines.append(((sk, ov, trn, shr), e, []))
+                                for ev in (a.env_values.split(";") if a.env_var else [None]):
+                                    if a.env_var:
+                                        if ev == "auto":
+                                            os.environ.pop(a.env_var, None)
+                                        else:
+                                            os.environ[a.env_var] = ev
+                                    e = rank_engine(pkg, n, rank, N, tp, a.handoff, ov, trn, hx)
+                                    e.init_random(1)
+                                    e.step(a.gens)
+                                    e.sync()
+                                    engines.append(((sk, ov, trn, shr, ev), e, []))
+                                if a.env_var:
+                                    os.environ.pop(a.env_var, None)
         os.environ.pop("GOL_DEV_AGE_SKEW", None)
         os.environ.pop("GOL_DEV_PASSES", None)
         os.environ.pop("GOL_DEV_RANK_SHRINK", None)
@@ -132,6 +143,7 @@ def main():
                               "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
                               "age_skew": e.age_skew, "skew_cfg": sk[0], "overlap_cfg": sk[1],
                               "transport": sk[2], "shrink_cfg": sk[3], "passes": e.passes,
+                              **({a.env_var: sk[4]} if a.env_var else {}),
                               "autotune": list(e.tuning),
                               "rank_tcups": round(rate, 2),
                               "aggregate_tcups_if_balanced": round(rate * N, 1),

@@ -174,6 +174,13 @@ def main():
                  "dur_old": round(statistics.median([float(dur_us[i]) for i in v if int(hw[i]) & 15 == 0] or [0]), 2),
                  "dur_young": round(statistics.median([float(dur_us[i]) for i in v if int(hw[i]) & 15 == 1] or [0]), 2)}
         for x, v in sorted(by_x.items())}
+    # (r06) does the workgroup -> XCC mapping follow round-robin (XCC = wg mod 8)?
+    # (the per-XCD row shift, GOL_DEV_XCD_SHIFT, assumes it for speed only)
+    rec["xcc_is_wg_mod8"] = round(sum(1 for i in range(len(w)) if int(hw[i]) >> 32 == int(wg[i]) % 8)
+                                  / max(1, len(w)), 4)
+    rec["xcc_of_wg_mod8"] = {str(m): dict(collections.Counter(int(hw[i]) >> 32 for i in range(len(w))
+                                                              if int(wg[i]) % 8 == m))
+                             for m in range(8)}
     print(json.dumps(rec), flush=True)
     e.close()
 
