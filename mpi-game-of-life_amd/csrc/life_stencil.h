@@ -71,33 +71,17 @@ namespace gol {
 
 namespace {
 
-// GOL_XLANE_LDS (dev A/B, tools/variant_build.sh): the lane shifts through the
-// LDS crossbar (ds_bpermute_b32, no VALU issue slot) plus one full-rate AND for
-// the zero fill, instead of the half-rate DPP move.
-#ifndef GOL_XLANE_LDS
-#define GOL_XLANE_LDS 0
-#endif
+// Lane shifts by DPP.  (r04: the LDS crossbar instead, ds_bpermute_b32 + a
+// full-rate AND for the zero fill, lost 25% at B/S2; removed in r06.)
 __device__ __forceinline__ uint32_t lane_from_left(uint32_t v)
 {
-#if GOL_XLANE_LDS
-    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 63) & 63) << 2, (int)v);
-    return r & (lane == 0 ? 0u : ~0u);
-#else
     // DPP wave_shr:1 -- lane l receives lane l-1's value; lane 0 receives 0.
     return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, true);
-#endif
 }
 __device__ __forceinline__ uint32_t lane_from_right(uint32_t v)
 {
-#if GOL_XLANE_LDS
-    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) << 2, (int)v);
-    return r & (lane == 63 ? 0u : ~0u);
-#else
     // DPP wave_shl:1 -- lane l receives lane l+1's value; lane 63 receives 0.
     return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xf, 0xf, true);
-#endif
 }
 
 // The NP 32-bit cell planes of one lane group (bitlayout.h): NP/2 words, 32*NP
@@ -148,50 +132,15 @@ __device__ __forceinline__ Grp<NP> load_grp(const uint64_t* p)
     return g;
 }
 // Field rows (written by an earlier launch, so plain loads would see them too).
-// Dev A/B (GOL_NT_LOADS=1): non-temporal loads (global_load ... nt).  A launch's
-// start needs every wavefront's first rows at once, and with the field larger
-// than the 256 MB Infinity Cache (65536^2) allocating loads took 12.8 us to
-// deliver 32 rows to every wavefront against 4.9 us for nt loads
-// (tools/burst_probe.hip, profiles/r05/burst_probe.jsonl).  In the kernel they
-// lost: 65536^2 156.7-156.9 vs 158.0-158.3 TCUPS, the 8-way rank 107.5-107.9 vs
-// 117.4-118.3 (the rows a block shares with its neighbours -- halo lanes of the
-// strips beside it, the rows around a block seam -- are no longer kept in L2);
-// nt stores beside them 111.6-111.7 (profiles/r05/ab_nt_loads_stores_rejected.jsonl).
-#ifndef GOL_NT_LOADS
-#define GOL_NT_LOADS 0
-#endif
-#ifndef GOL_NT_STORES
-#define GOL_NT_STORES 0
-#endif
+// (r05: non-temporal loads and stores -- all of them, or the warm-up rows only --
+// shortened the start burst but lost in the kernel, 65536^2 156.7-156.9 vs
+// 158.0-158.3 TCUPS, the 8-way rank 107.5-107.9 vs 117.4-118.3: the rows a block
+// shares with its neighbours no longer stay in L2; nt stores 111.6-111.7;
+// profiles/r05/ab_nt_loads_stores_rejected.jsonl.  The switches were removed in r06.)
 template <int NP>
 __device__ __forceinline__ Grp<NP> load_field(const uint64_t* p)
 {
-#if GOL_NT_LOADS
-    Grp<NP> g;
-#pragma unroll
-    for (int i = 0; i < NP / 2; ++i) g.w[i] = __builtin_nontemporal_load(p + i);
-    return g;
-#else
     return load_grp<NP>(p);
-#endif
-}
-
-// Dev A/B (GOL_NT_WARM=1): non-temporal loads for the warm-up rows loaded up front
-// only (the start burst), the steady stream allocating as usual.
-#ifndef GOL_NT_WARM
-#define GOL_NT_WARM 0
-#endif
-template <int NP>
-__device__ __forceinline__ Grp<NP> load_warm(const uint64_t* p)
-{
-#if GOL_NT_WARM
-    Grp<NP> g;
-#pragma unroll
-    for (int i = 0; i < NP / 2; ++i) g.w[i] = __builtin_nontemporal_load(p + i);
-    return g;
-#else
-    return load_field<NP>(p);
-#endif
 }
 
 template <int NP>
@@ -504,10 +453,7 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 #define GOL_EXP 0
 #endif
 // (r05) warm-up rows loaded up front (see the kernel); 0 = the r04 one-block ring
-#ifndef GOL_WARM_PREFETCH
-#define GOL_WARM_PREFETCH 1
-#endif
-// (r05) The warm-up's first GOL_WARM_AHEAD rows are loaded up front and each
+// (r05) The warm-up's first kWarmAheadRows rows are loaded up front and each
 // warm-up block issues the rows that many steps ahead of it, with a scheduling
 // barrier between the blocks that keeps those loads where they are.  Every
 // wavefront of a launch starts at once and its first loads stall at issue on the
@@ -517,13 +463,12 @@ constexpr int kWarmBlk = 0, kPure = 1, kSide = 2, kPureMask = 3;
 // (profiles/r05/ab_warm_ahead.jsonl), mean TCUPS of own rows, all 32 rows up
 // front / 16 / 12 / 8 ahead: 8-way 117.8 / 118.4-118.9 / 118.9 / 119.7, 4-way
 // 136.0 / 136.1-136.4 / 137.1 / 136.8; 65536^2 157.8-158.0 (16) vs 158.1-158.2
-// (8).  0 = every warm-up row up front.
-#ifndef GOL_WARM_AHEAD
-#define GOL_WARM_AHEAD 8
-#endif
-#ifndef GOL_WARM_BARRIER
-#define GOL_WARM_BARRIER 1
-#endif
+// (8).  (The r04 one-block ring and these dev switches were removed in r06.)
+constexpr int kWarmAheadRows = 8;
+// the steady ring's first rows are issued this many warm-up blocks before the
+// steady loop (r05: 1 or 3 instead of 2 measured no better,
+// profiles/r05/ab_steady_lead_rejected.jsonl)
+constexpr int kSteadyLeadBlocks = 2;
 
 // MP: the multi-pass form (StepArgs::npass > 1; a separate instantiation, so the
 // single-pass kernel's steady loop stays exactly as it was)
@@ -542,8 +487,7 @@ void life_tb_kernel(StepArgs a)
     constexpr int kPrefetch = kPfOf<NP, K>();
     constexpr int kSideRows = 2 * (K - 1);  // hand-off rows per block: 2 per generation 1..K-1
     constexpr int kWarmSteps = (2 * K + kPrefetch - 1) / kPrefetch * kPrefetch;  // unrolled warm-up
-    constexpr int kWarmAhead =
-        (GOL_WARM_AHEAD > 0 && GOL_WARM_AHEAD < kWarmSteps) ? GOL_WARM_AHEAD : kWarmSteps;
+    constexpr int kWarmAhead = kWarmAheadRows < kWarmSteps ? kWarmAheadRows : kWarmSteps;
     static_assert(K + 2 * kPrefetch <= kGuardRows, "streaming loads must stay in the guard rows");
     static_assert(!HAND || K >= kHandoffMinDepth, "hand-off kernels start at kHandoffMinDepth");
     static_assert(TOFF >= 0 && TOFF < kPrefetch && (HAND || TOFF == 0), "tail offset");
@@ -876,31 +820,20 @@ void life_tb_kernel(StepArgs a)
             dn_side + (int64_t)(s - t_side) * kSideRowBytes + voff_side));
     };
     Grp<NP> ring[kPrefetch];
-#if GOL_WARM_PREFETCH
-    // (r05) Every row of the unrolled warm-up is loaded up front, and the steady
-    // ring two warm-up blocks before the steady loop.  With the one-block ring
-    // the compiler pulled each warm-up block's ingest up into the block before
-    // (no scheduling barriers there), so every refill was consumed right after
-    // its issue: a chain of HBM round trips (s_waitcnt vmcnt(0/1) after each
-    // load) that made the 2K warm-up steps take 16-20 us per wavefront at every
-    // shape (profiles/r05/wave_phases_*.jsonl).
-    // (dev A/B, GOL_WARM_AHEAD = n: only the first n warm-up rows up front, each
-    // warm-up block issuing the rows n steps ahead of it)
+    // (r05) The warm-up rows have a ring of their own (the first kWarmAhead loaded
+    // up front, each warm-up block issuing the rows kWarmAhead steps ahead), and
+    // the steady ring is filled kSteadyLeadBlocks warm-up blocks before the steady
+    // loop.  With the r04 one-block ring the compiler pulled each warm-up block's
+    // ingest up into the block before (no scheduling barriers there), so every
+    // refill was consumed right after its issue: a chain of HBM round trips
+    // (s_waitcnt vmcnt(0/1) after each load) that made the 2K warm-up steps take
+    // 16-20 us per wavefront at every shape (profiles/r05/wave_phases_*.jsonl).
     Grp<NP> wring[kWarmSteps];
 #pragma unroll
     for (int p = 0; p < kWarmAhead; ++p)  // (input rows: t_side >= warm-up + 2 blocks)
-        wring[p] = load_warm<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)p * rs + voff_ld));
-    // (the steady ring's first rows: issued GOL_STEADY_LEAD warm-up blocks before the
-    // steady loop; dev A/B)
-#ifndef GOL_STEADY_LEAD
-#define GOL_STEADY_LEAD 2
-#endif
+        wring[p] = load_field<NP>(reinterpret_cast<const uint64_t*>(in_rows + (int64_t)p * rs + voff_ld));
     constexpr int kSteadyIssue =
-        kWarmSteps >= GOL_STEADY_LEAD * kPrefetch ? kWarmSteps - GOL_STEADY_LEAD * kPrefetch : 0;
-#else
-#pragma unroll
-    for (int p = 0; p < kPrefetch; ++p) ring[p] = load_step(p);
-#endif
+        kWarmSteps >= kSteadyLeadBlocks * kPrefetch ? kWarmSteps - kSteadyLeadBlocks * kPrefetch : 0;
 #if GOL_EXP & 16384
     // dev probe of a wavefront's start (tools/wave_log.py --probe): the initial
     // loads issued, and all of them landed (results stay valid, timing does not)
@@ -974,14 +907,7 @@ void life_tb_kernel(StepArgs a)
             if (wt) {
                 store_side<NP>(reinterpret_cast<uint64_t*>(o), x);
             } else {
-#if GOL_NT_STORES
-                const Grp<NP> g = words_of(x);
-#pragma unroll
-                for (int i = 0; i < NP / 2; ++i)
-                    __builtin_nontemporal_store(g.w[i], reinterpret_cast<uint64_t*>(o) + i);
-#else
                 *reinterpret_cast<Grp<NP>*>(o) = words_of(x);
-#endif
             }
         }
     };
@@ -1080,8 +1006,7 @@ void life_tb_kernel(StepArgs a)
         // births masked everywhere but in kPure blocks (t_plain_end)
         constexpr bool kMask = kBirths && kMode != kPure;
         Pl<NP> x[kPrefetch];
-#if GOL_WARM_PREFETCH
-        if constexpr (kGuard && GOL_WARM_BARRIER) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kGuard) __builtin_amdgcn_sched_barrier(0);
         if constexpr (kGuard) {
 #pragma unroll
             for (int p = 0; p < kPrefetch; ++p) {
@@ -1091,7 +1016,6 @@ void life_tb_kernel(StepArgs a)
                 if (t0 == kSteadyIssue) ring[p] = load_in(kWarmSteps + p);
             }
         } else
-#endif
 #pragma unroll
         for (int p = 0; p < kPrefetch; ++p) {
             x[p] = ingest(t0 + p, ring[p], std::integral_constant<bool, kSideMode>{});
