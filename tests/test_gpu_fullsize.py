@@ -146,3 +146,30 @@ def test_conway_16384_1000_generations_vs_oracle(pkg, oracle):
         got = e.digest()
     g = oracle.bp_run(oracle.bp_random(n, n, 3), n, 1000, oracle.CONWAY, threads=THREADS)
     assert got == oracle.bp_digest(g, n)
+
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_c4_group_vs_oracle(pkg, oracle, nranks):
+    """(r06) The C4 partition against the oracle itself, not only against the
+    single engine: 65536^2 in 2 / 4 / 8 row stripes (gol_rank_rows), default K = 16
+    and Hx (192 / 192 / 128), one full halo round and a partial one (Hx + 16
+    generations, B3/S23 so births cross every stripe seam).  After G generations a row depends only on
+    the rows within G of it, so the oracle evolves a band of +-(G + 32) rows
+    around each stripe seam (and around one row in the middle of each stripe) with
+    a dead border and its middle 64 rows are the exact global rows there: those
+    are compared bytewise with the stripes' stored rows."""
+    hx = 128 if nranks == 8 else 192
+    G, half = hx + 16, 32
+    with pkg.Group(N, N, nranks, rule=pkg.CONWAY) as grp:
+        assert (grp.members[0].tb_depth, grp.members[0].halo_depth) == (16, hx)
+        seams = [m.row0 for m in grp.members[1:]]
+        mids = [m.row0 + m.rows // 2 for m in grp.members]
+        grp.init_random(6)
+        grp.step(G)
+        got = grp.store_packed()
+    g0 = oracle.bp_random(N, N, 6)
+    for r in seams + mids + [0, N - half]:
+        lo, hi = max(0, r - half - G), min(N, r + half + G)
+        band = oracle.bp_run(g0[lo:hi], N, G, oracle.CONWAY, threads=THREADS)
+        a, b = max(0, r - half), min(N, r + half)
+        assert (got[a:b] == band[a - lo:b - lo]).all(), f"rows [{a}, {b})"
