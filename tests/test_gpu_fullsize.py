@@ -13,6 +13,7 @@ stripes on 2 streams, 256-row halo rounds) is checked the same way.  Checked
 Bit-exact (integer work): digests (live count + order-independent 64-bit hash)
 must be equal.
 """
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -173,3 +174,25 @@ def test_c4_group_vs_oracle(pkg, oracle, nranks):
         band = oracle.bp_run(g0[lo:hi], N, G, oracle.CONWAY, threads=THREADS)
         a, b = max(0, r - half), min(N, r + half)
         assert (got[a:b] == band[a - lo:b - lo]).all(), f"rows [{a}, {b})"
+
+
+def test_c5_group_vs_oracle_at_seams(pkg, oracle):
+    """(r06) The C5 partition, 262144^2 in 8 stripes of 32768 rows (Hx = 192,
+    device-copy exchanges; 8 GiB per field buffer in all), on one GPU as an
+    in-process group: one full halo round and a partial one (208 generations of
+    B3/S23), checked against the oracle in light-cone bands around every stripe
+    seam (the oracle builds only those rows of the splitmix64 field)."""
+    n, half = 262144, 32
+    with pkg.Group(n, n, 8, rule=pkg.CONWAY) as grp:
+        m0 = grp.members[0]
+        assert (m0.rows, m0.tb_depth, m0.halo_depth) == (32768, 16, 192)
+        G = m0.halo_depth + 16
+        grp.init_random(8)
+        grp.step(G)
+        for up, dn in zip(grp.members, grp.members[1:]):
+            s = dn.row0
+            got = np.concatenate([up.store_packed()[-half:], dn.store_packed()[:half]])
+            lo, hi = s - half - G, s + half + G
+            band = oracle.bp_run(oracle.bp_random_rows(lo, hi - lo, n, 8), n, G, oracle.CONWAY,
+                                 threads=THREADS)
+            assert (got == band[G:G + 2 * half]).all(), f"seam at row {s}"
