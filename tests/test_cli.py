@@ -82,6 +82,24 @@ def test_cli_conway_rule(pkg, oracle, tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_c2_program_surface(pkg, oracle, tmp_path):
+    """(r06) C2 through the reference's program surface: a 4096 x 4096 data.txt
+    (16.8 MB, the splitmix64 p = 0.5 field) and 1000 epochs in
+    grid_size_data.txt; the CLI's output.txt (GPU ASCII codec in and out, the
+    resident kernel between) equals the oracle's 1000 generations byte for byte."""
+    n = 4096
+    g = oracle.bp_random(n, n, 1)
+    d = setup_dir(tmp_path, 1000, n, n, oracle.bp_unpack(g, n))
+    r = run_cli(pkg, d)
+    assert r.returncode == 0, r.stderr
+    want = oracle.bp_unpack(oracle.bp_run(g, n, 1000, oracle.REF_RULE, threads=16), n)
+    assert (d / "output.txt").read_bytes() == want
+    lines = r.stdout.splitlines()
+    assert lines[0] == "Process 0 wrote data to the file."
+    assert re.fullmatch(r"Total time = [0-9.e+-]+", lines[1])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("stripes", [2, 5])
 def test_cli_stripes_intended_semantics(pkg, tmp_path, stripes):
     """--stripes S (S row stripes with real halo exchange, one process) gives the
