@@ -11,6 +11,7 @@
 #   bench:NAME[:ARGS]   python bench.py ARGS -> NAME.json
 #   rehearse2:NAME[:ARGS]  bench.py --gpus 2 on ONE GPU with self-looped RCCL
 #                       (GOL_DEV_RCCL_SELF=1, ranks over gloo) -> NAME.json
+#   rehearse8:NAME[:ARGS]  the same with 8 ranks sharing the one GPU
 #   proxy:NAME:ARGS     python tools/rank_proxy.py ARGS -> NAME.jsonl
 #   py:NAME:ARGS        python ARGS (a tool script and its arguments) -> NAME.out
 #   trace:NAME:CMD      rocprofv3 --kernel-trace --stats of python CMD -> NAME/
@@ -47,6 +48,12 @@ for step in "$@"; do
     rehearse2)
       GOL_DEV_RCCL_SELF=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
+          $args > "$OUT/$name.json" 2> "$OUT/$name.err" \
+          || { grep -A3 Error "$OUT/$name.err" | head -30; exit 5; }
+      cut -c1-600 "$OUT/$name.json" ;;
+    rehearse8)
+      GOL_DEV_RCCL_SELF=1 timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 8 \
           $args > "$OUT/$name.json" 2> "$OUT/$name.err" \
           || { grep -A3 Error "$OUT/$name.err" | head -30; exit 5; }
       cut -c1-600 "$OUT/$name.json" ;;
