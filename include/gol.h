@@ -102,8 +102,11 @@ typedef struct gol_config {
                               field fits (then tb_depth sets K and rows_per_wave
                               the rows each wavefront holds: 2,3,4,6,8) */
     uint32_t exchange_overlap; /* rank engines and groups: 0 = auto (rank engines
-                              exchange after the round's last launch, blocking;
-                              in-process groups overlap), 1 = blocking, 2 =
+                              over RCCL time both modes at create on their
+                              communicator and keep the faster, the same on
+                              every rank: gol_plan_exchange; rank engines over a
+                              host transport block; in-process groups overlap),
+                              1 = blocking, 2 =
                               overlapped (the round's last launch splits into a
                               band launch of the rows the neighbours need and an
                               interior launch, and the exchange of the band rows
@@ -254,6 +257,18 @@ gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint3
  * *tuned_us / *model_us = the best create-time launch of the plan that runs / of
  * the models' plan (0 when nothing was timed).  Out pointers may be NULL. */
 gol_status gol_plan_tuning(gol_engine* e, uint32_t* variant, float* tuned_us, float* model_us);
+
+/* (r07) Exchange mode of a stripe engine: *mode = 1 blocking (the exchange after
+ * the round's last launch), 2 overlapped (band launch, then the exchange beside
+ * the interior launch), 0 for an engine without halo exchanges.  With
+ * exchange_overlap = 0 a rank engine over RCCL chooses it at create by timing
+ * rounds of both modes on its communicator (a collective: every rank of the job
+ * runs the same rounds); *blocking_ms / *overlapped_ms are then the max over ranks
+ * of each mode's best time per round, else 0.  gol_round_schedule called with
+ * exchange_overlap set to *mode lists what gol_step runs.  Out pointers may be
+ * NULL. */
+gol_status gol_plan_exchange(gol_engine* e, uint32_t* mode, float* blocking_ms,
+                             float* overlapped_ms);
 
 /* Passes per full-depth launch of the first full-depth plan: 1, or 2-3 for
  * multi-pass launches (each launch runs that many depth-K passes over its row

@@ -36,7 +36,7 @@ EXPORTS = [
     "gol_create_rank_transport", "gol_round_schedule", "gol_plan_handoff",
     "gol_plan_resident", "gol_plan_skew", "gol_plan_columns", "gol_plan_tuning",
     "gol_digest_rows", "gol_comm_info", "gol_plan_model", "gol_plan_passes",
-    "gol_plan_resident_rows",
+    "gol_plan_resident_rows", "gol_plan_exchange",
 ]
 
 # gol_plan_tuning's variants (engine.cpp kTuneVariantNames): 0 = the models' plan
@@ -184,6 +184,7 @@ def lib():
     pf32 = ctypes.POINTER(ctypes.c_float)
     L.gol_plan_tuning.argtypes = [vp, ctypes.POINTER(u32), pf32, pf32]
     L.gol_plan_passes.argtypes = [vp, ctypes.POINTER(u32)]
+    L.gol_plan_exchange.argtypes = [vp, ctypes.POINTER(u32), pf32, pf32]
     L.gol_plan_resident_rows.argtypes = [vp] + [ctypes.POINTER(u32)] * 4
     L.gol_digest_rows.argtypes = [vp, u64, u64, pu64, pu64]
     pi32 = ctypes.POINTER(ctypes.c_int)
@@ -201,7 +202,7 @@ def lib():
                  "gol_plan_resident", "gol_plan_skew", "gol_plan_columns",
                  "gol_create_rank_transport", "gol_round_schedule", "gol_plan_tuning",
                  "gol_digest_rows", "gol_comm_info", "gol_plan_model", "gol_plan_passes",
-                 "gol_plan_resident_rows"]:
+                 "gol_plan_resident_rows", "gol_plan_exchange"]:
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -347,6 +348,13 @@ class Engine:
         np_ = ctypes.c_uint32()
         _check(lib().gol_plan_passes(self._h, ctypes.byref(np_)))
         self.passes = np_.value  # passes per full-depth launch (multi-pass launches)
+        xm, xb, xo = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_float()
+        _check(lib().gol_plan_exchange(self._h, ctypes.byref(xm), ctypes.byref(xb), ctypes.byref(xo)))
+        # exchange mode of a stripe engine ("blocking" / "overlapped", None without
+        # exchanges) and, when it was chosen by timing at create (exchange_overlap =
+        # 0 over RCCL), the max over ranks of each mode's best ms per round
+        self.exchange = ({1: "blocking", 2: "overlapped"}.get(xm.value),
+                         round(xb.value, 4), round(xo.value, 4))
 
     def close(self):
         if self._h:

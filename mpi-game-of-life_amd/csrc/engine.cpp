@@ -151,15 +151,17 @@ struct Region {
 // round (c = 1..Hx); with overlap, plans[Hx] (band: the rows the neighbours need)
 // and plans[Hx+1] (interior) split the round's last launch.  Shared by the rank
 // engines and gol_round_schedule, so the exported schedule is the one run.
+// `overlap`: the mode the schedule starts in; `band`: the band and interior plans
+// exist (overlap, or an exchange mode to be chosen by timing: `tune`).
 struct RankGeom {
     uint64_t row0 = 0, R = 0, Hx = 0, buf_rows = 0;
     uint32_t K = 8;
-    bool overlap = false;
+    bool overlap = false, band = false, tune = false;
     std::vector<std::vector<SegDesc>> raw;
 };
 
 gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks, RankGeom* g,
-                         bool group = false);
+                         bool group = false, bool tune_ok = false);
 
 }  // namespace
 
@@ -215,8 +217,14 @@ struct gol_engine {
     // few wavefronts to fill the GPU.
     hipStream_t comm_stream = nullptr, band_stream = nullptr;
     hipEvent_t ev_band = nullptr, ev_xdone = nullptr, ev_in = nullptr, ev_join = nullptr;
-    bool overlap = false;
+    bool overlap = false;     // the mode gol_step runs (RankGeom::overlap at create)
+    bool band_plans = false;  // the band and interior plans exist (RankGeom::band)
     bool halo_fresh = false;
+    // (r07) exchange_overlap = 0 on a rank engine over RCCL: both modes timed at
+    // create (tune_exchange), the max over ranks of each mode's best sample (ms);
+    // 0 = not timed
+    bool xchg_tune = false;
+    float xchg_ms[2] = {0.f, 0.f};  // blocking, overlapped
 
     // composite engine (gol_create, large GLOBAL fields): the field is S row
     // stripes on S streams of this device (a gol_create_group), so one stripe's
@@ -808,8 +816,8 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         p.segs = r;
         // the band launch runs beside the interior launch: classic blocks, so that
         // at most one launch that waits for its own wavefronts runs at a time
-        const bool band = e->overlap && pi == (size_t)e->Hx;
-        const bool inner = e->overlap && pi == (size_t)e->Hx + 1;
+        const bool band = e->band_plans && pi == (size_t)e->Hx;
+        const bool inner = e->band_plans && pi == (size_t)e->Hx + 1;
         const RowPlan rp = pick_rows_per_wave(r, e->ng, (int)e->K, e->planes, occ_c, occ_h, 4 * cus,
                                               (int)e->rows_per_wave, e->lane_shift,
                                               band ? 1u : kind, hs_v);
@@ -994,7 +1002,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         // rows already planned (rank engines: the full-depth launches of a round
         // share one region, rank_geometry): the same plan, resolved after the
         // autotuner (resolve_aliases)
-        const bool role = e->overlap && pi >= (size_t)e->Hx;  // band / interior
+        const bool role = e->band_plans && pi >= (size_t)e->Hx;  // band / interior
         for (size_t pj = 0; pj < pi && !role; ++pj) {
             if (e->plan_alias[pj] >= 0 || raw[pj].size() != raw[pi].size()) continue;
             bool same = true;
@@ -1059,7 +1067,7 @@ gol_status build_plans(gol_engine* e, const std::vector<std::vector<SegDesc>>& r
         // (multi-pass: hand-off slots and flags per pass parity)
         const size_t slot = (size_t)2 * (e->K - 1) * 64 * (size_t)(e->planes / 2);
         const size_t par = any_mp ? 2 : 1;
-        const int regions = e->overlap ? 2 : 1;
+        const int regions = e->band_plans ? 2 : 1;
         for (int r = 0; r < regions; ++r) {
             HIP_TRY(hipMalloc(&e->side[r], par * (size_t)max_units * slot * sizeof(uint64_t)));
             HIP_TRY(hipMalloc(&e->flags[r], par * (size_t)max_units * sizeof(uint32_t)));
@@ -1106,7 +1114,7 @@ gol_status check_cfg(const gol_config* cfg)
 }
 
 gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks, RankGeom* g,
-                         bool group)
+                         bool group, bool tune_ok)
 {
     gol_status st = gol_rank_rows(h, nranks, rank, &g->row0, &g->R);
     if (st != GOL_OK) return st;
@@ -1140,7 +1148,7 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
     g->Hx = nranks > 1 ? Hx : 0;
     g->raw.clear();
-    g->overlap = false;
+    g->overlap = g->band = g->tune = false;
     if (nranks <= 1) {
         g->buf_rows = h;
         return GOL_OK;
@@ -1188,16 +1196,24 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // build_plans) the band does run concurrently (trace_rank8_overlap_capped.csv),
     // but per-rank rates through the host-transport proxy stayed within -3..+3% of
     // blocking and bimodal at 2 ranks, and an RCCL exchange is itself a kernel that
-    // needs free slots: blocking stays the rank default.  gol_config.exchange_overlap
-    // chooses either mode (bench.py --gpus N times both); with it at 0 (auto),
-    // GOL_DEV_OVERLAP = 1 / 0 forces the overlap on / off (dev A/B).
+    // needs free slots: blocking was the rank default through r06, measured on the
+    // RCCL self-loop, where the exchange is a device-local copy.  Over xGMI the
+    // exchange costs more and may be worth hiding, so (r07) with
+    // gol_config.exchange_overlap = 0 a rank engine over RCCL (tune_ok) builds both
+    // schedules' plans, starts blocking, and gol_create_rank times both modes on
+    // the real communicator and keeps the faster (tune_exchange).
+    // gol_config.exchange_overlap = 1 / 2 forces a mode (bench.py --gpus N times
+    // both); with it at 0, GOL_DEV_OVERLAP = 1 / 0 forces the overlap on / off (dev
+    // A/B).
     const int64_t Hx_ = (int64_t)g->Hx, R = (int64_t)g->R;
-    bool want = group;
+    bool want = group, tune = false;
     if (cfg->exchange_overlap)
         want = cfg->exchange_overlap == 2;
     else if (const char* ov = std::getenv("GOL_DEV_OVERLAP"))
         want = ov[0] == '1';
-    if ((int64_t)(h / (uint64_t)nranks) >= 2 * Hx_ && want) {
+    else
+        tune = tune_ok;
+    if ((int64_t)(h / (uint64_t)nranks) >= 2 * Hx_ && (want || tune)) {
         SegDesc b = g->raw.back()[0];  // shrink Hx: out = own rows
         std::vector<SegDesc> band, inner;
         int64_t ilo = Hx_, ihi = Hx_ + R;
@@ -1221,7 +1237,9 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
         inner.push_back(t);
         g->raw.push_back(band);
         g->raw.push_back(inner);
-        g->overlap = true;
+        g->overlap = want;
+        g->band = true;
+        g->tune = tune;
     }
     return GOL_OK;
 }
@@ -1366,6 +1384,8 @@ gol_status raw_regions(gol_engine* e, uint64_t h, const gol_config* cfg, const R
     if (e->nranks > 1) {
         e->buf_rows = geom->buf_rows;
         e->overlap = geom->overlap;
+        e->band_plans = geom->band;
+        e->xchg_tune = geom->tune;
         raw = geom->raw;
         e->user_regions.push_back({e->Hx, e->row0, 0, e->R});
         e->load_regions = e->user_regions;
@@ -2312,7 +2332,8 @@ namespace {
 
 // Geometry + device state of stripe `rank` of `nranks` (no transport yet).
 gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int rank, int nranks,
-                            gol_engine** out, bool shared_device = false, bool group = false)
+                            gol_engine** out, bool shared_device = false, bool group = false,
+                            bool tune_ok = false)
 {
     *out = nullptr;
     gol_status st = check_cfg(cfg);
@@ -2321,7 +2342,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
         return fail(GOL_EINVAL, "rank engines implement GLOBAL semantics only");
     if (h == 0 || w == 0) return fail(GOL_EINVAL, "h and w must be >= 1");
     RankGeom g;
-    st = rank_geometry(h, cfg, rank, nranks, &g, group);
+    st = rank_geometry(h, cfg, rank, nranks, &g, group, tune_ok);
     if (st != GOL_OK) return st;
     gol_engine* e = new (std::nothrow) gol_engine();
     if (!e) return fail(GOL_ENOMEM, "host allocation");
@@ -2349,6 +2370,71 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     return GOL_OK;
 }
 
+// (r07) gol_config.exchange_overlap = 0 on a rank engine over RCCL: time both
+// exchange modes on this communicator -- blocking (after the round's last launch)
+// and overlapped (band launch, then the exchange on the comm stream beside the
+// interior launch) -- and keep the faster.  Both schedules are bit-exact (the
+// parity tests run each one); only the time differs, and that depends on what an
+// exchange costs: a device-local copy on the RCCL self-loop of a one-GPU box, an
+// xGMI transfer plus RCCL's kernels between two MI355X.  Every rank runs the same
+// sequence (the same geometry, generations and modes, so its exchanges pair up),
+// and the max over ranks of each mode's best sample decides (ncclAllReduce), so all
+// ranks keep one mode.  Overlapped must be kXchgMargin faster (samples scatter by
+// ~1%).  Like the plan autotuner: on a p = 0.5 field, zeroed again afterwards.
+constexpr float kXchgMargin = 0.99f;
+
+gol_status tune_exchange(gol_engine* e)
+{
+    if (!e->xchg_tune || !e->band_plans || e->xfer != XFER_RCCL) return GOL_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t words_all = (size_t)(e->buf_rows + 2 * gol::kGuardRows) * e->stride;
+    HIP_TRY(gol::launch_init_random(e->buf[e->cur], (int64_t)e->stride, (int64_t)e->wq,
+                                    e->lastmask, 0, 0, (int64_t)e->buf_rows, 0x5eedull,
+                                    e->planes, e->stream));
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    HIP_TRY(hipEventCreate(&t0));
+    HIP_TRY(hipEventCreate(&t1));
+    // samples of 4 rounds (the last overlapped exchange of a sample is exposed by
+    // the join, as at the end of a caller's step); one untimed pass of both modes
+    constexpr int kReps = 2, kRounds = 4;
+    float best[2] = {1e30f, 1e30f};
+    gol_status st = GOL_OK;
+    for (int rep = 0; rep <= kReps && st == GOL_OK; ++rep)
+        for (int m = 0; m < 2 && st == GOL_OK; ++m) {
+            e->overlap = m == 1;  // (a pending overlapped exchange is waited for first)
+            float ms = 0;
+            if (hipEventRecord(t0, e->stream) != hipSuccess) st = fail(GOL_EHIP, "exchange tuning event");
+            if (st == GOL_OK) st = gol_step(e, (uint64_t)kRounds * e->Hx);
+            if (st == GOL_OK) st = join_side_streams(e);
+            if (st == GOL_OK && (hipEventRecord(t1, e->stream) != hipSuccess ||
+                                 hipEventSynchronize(t1) != hipSuccess ||
+                                 hipEventElapsedTime(&ms, t0, t1) != hipSuccess))
+                st = fail(GOL_EHIP, "exchange tuning timing");
+            if (rep > 0) best[m] = std::min(best[m], ms);
+        }
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    e->overlap = false;
+    if (st == GOL_OK) st = quiesce(e);
+    if (st == GOL_OK) st = check_err(e);
+    if (st != GOL_OK) return st;
+    float agreed[2] = {best[0], best[1]};
+    HIP_TRY(hipMemcpy(e->d_acc, agreed, sizeof agreed, hipMemcpyHostToDevice));
+    NCCL_TRY(ncclAllReduce(e->d_acc, e->d_acc, 2, ncclFloat32, ncclMax, e->comm, e->stream));
+    HIP_TRY(hipMemcpyAsync(agreed, e->d_acc, sizeof agreed, hipMemcpyDeviceToHost, e->stream));
+    for (int b = 0; b < e->nbuf; ++b)
+        HIP_TRY(hipMemsetAsync(e->alloc[b], 0, words_all * sizeof(uint64_t), e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->xchg_ms[0] = agreed[0] / kRounds;
+    e->xchg_ms[1] = agreed[1] / kRounds;
+    e->overlap = agreed[1] < kXchgMargin * agreed[0];
+    e->halo_fresh = false;
+    if (std::getenv("GOL_DEV_PLANS"))
+        std::fprintf(stderr, "exchange mode: %s (blocking %.3f ms, overlapped %.3f ms per round)\n",
+                     e->overlap ? "overlapped" : "blocking", e->xchg_ms[0], e->xchg_ms[1]);
+    return GOL_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2358,7 +2444,7 @@ gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int ra
 {
     if (!out || !id) return fail(GOL_EINVAL, "null argument");
     gol_engine* e = nullptr;
-    gol_status st = make_rank_engine(h, w, cfg, rank, nranks, &e);
+    gol_status st = make_rank_engine(h, w, cfg, rank, nranks, &e, false, false, true);
     if (st != GOL_OK) return st;
     if (nranks > 1) {
         ncclUniqueId u;
@@ -2394,6 +2480,13 @@ gol_status gol_create_rank(uint64_t h, uint64_t w, const gol_config* cfg, int ra
             return fail(GOL_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
         }
         e->xfer = XFER_RCCL;
+        st = tune_exchange(e);
+        if (st != GOL_OK) {
+            std::string msg = g_last_error;
+            gol_destroy(e);
+            g_last_error = msg;
+            return st;
+        }
     }
     *out = e;
     return GOL_OK;
@@ -3172,6 +3265,16 @@ gol_status gol_plan_tuning(gol_engine* e, uint32_t* variant, float* tuned_us, fl
     return GOL_OK;
 }
 
+gol_status gol_plan_exchange(gol_engine* e, uint32_t* mode, float* blocking_ms, float* overlapped_ms)
+{
+    if (!e) return fail(GOL_EINVAL, "null engine");
+    const gol_engine* s = e->parts.empty() ? e : e->parts[0];
+    if (mode) *mode = s->nranks > 1 ? (s->overlap ? 2u : 1u) : 0u;
+    if (blocking_ms) *blocking_ms = s->xchg_ms[0];
+    if (overlapped_ms) *overlapped_ms = s->xchg_ms[1];
+    return GOL_OK;
+}
+
 gol_status gol_plan_passes(gol_engine* e, uint32_t* passes)
 {
     if (!e || !passes) return fail(GOL_EINVAL, "null argument");
@@ -3278,9 +3381,13 @@ gol_status gol_info(gol_engine* e, uint64_t* h, uint64_t* w, uint64_t* row0, uin
         if (rows) *rows = e->H;
         return GOL_OK;
     }
+    // (rank engines: plans[Hx-1], the round's full-depth launch; the band and
+    // interior plans come after it)
+    const size_t full = (e->nranks > 1 && e->Hx >= 1 && e->plans.size() >= e->Hx) ? e->Hx - 1
+                                                                                   : e->plans.size() - 1;
     if (rows_per_wave)
         *rows_per_wave = e->res.on ? (uint32_t)e->res.rows
-                                   : e->plans.empty() ? 0 : (uint32_t)e->plans.back().rpw;
+                                   : e->plans.empty() ? 0 : (uint32_t)e->plans[full].rpw;
     if (h) *h = e->H;
     if (w) *w = e->W;
     if (row0) *row0 = e->row0;

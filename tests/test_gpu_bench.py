@@ -41,3 +41,29 @@ def test_bench_json_contract():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k
     assert cb["cores"] == 2 and cb["kind"] == "port" and cb["value"] > 0
+
+
+def test_bench_two_rank_rehearsal_exchange_modes():
+    """bench.py --gpus 2 under torch.distributed.run on ONE GPU (GOL_DEV_RCCL_SELF=1:
+    each rank's engine talks RCCL to itself, ranks over gloo): the N > 1 record
+    carries both forced exchange modes and the default engine's own choice (r07),
+    and a rehearsal never reports an N-GPU value."""
+    env = dict(os.environ, GOL_DEV_RCCL_SELF="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", "29561", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--size", "8192", "--gens", "256", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=280, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["rehearsal"] is True and rec["value"] is None
+    modes = rec["exchange_modes"]
+    assert set(modes) == {"overlapped", "blocking", "auto"}
+    auto = modes["auto"]
+    assert auto["default"] is True and auto["mode"] in ("blocking", "overlapped")
+    assert rec["config"]["exchange"] == auto["mode"]
+    assert all(v > 0 for v in auto["tuned_ms_per_round"].values())
+    for m in modes.values():
+        assert m["value"] > 0 and len(m["per_rank"]) == 2

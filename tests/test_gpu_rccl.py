@@ -180,6 +180,43 @@ def test_rank_timing_spans_add_up(pkg, monkeypatch, overlap):
     assert t["round_ms"] + t["exchange_exposed_ms"] <= wall * 1.01 + 0.05, (t, wall)
 
 
+@pytest.mark.parametrize("world,rank,size", [(4, 1, 4096), (8, 3, 65536)])
+def test_rccl_exchange_mode_chosen_at_create(pkg, monkeypatch, world, rank, size):
+    """exchange_overlap = 0 (r07): a rank engine over RCCL times rounds of both
+    exchange modes at create on its communicator (engine.cpp tune_exchange; the
+    self-loop here, xGMI between two MI355X) and keeps the faster.  Whichever it
+    keeps, its field equals the host loopback transport's (which blocks) bytewise
+    over full rounds, partial ones and a carried overlapped exchange; the choice
+    follows the reported timings; forced modes report themselves untimed."""
+    monkeypatch.setenv("GOL_DEV_RCCL_SELF", "1")
+    chunks = None
+    out = []
+    for mode in ("rccl", "host"):
+        kw = dict(uid=pkg.unique_id()) if mode == "rccl" else dict(transport=lambda su, sd: (su, sd))
+        with pkg.Engine(size, size, rule=pkg.CONWAY, device=0, rank=rank, nranks=world, **kw) as e:
+            if mode == "rccl":
+                chosen, tb, to = e.exchange
+                assert chosen in ("blocking", "overlapped") and tb > 0 and to > 0, e.exchange
+                if abs(to - 0.99 * tb) > 1e-3 * tb:  # (the rounded report at the margin)
+                    assert (chosen == "overlapped") == (to < 0.99 * tb), e.exchange
+            else:
+                assert e.exchange == ("blocking", 0.0, 0.0)
+            hx = e.halo_depth
+            chunks = [hx, 7, 2 * hx + 3]
+            e.init_random(11)
+            res = []
+            for c in chunks:
+                e.step(c)
+                res.append((e.digest(), e.store_packed()))
+        out.append(res)
+    for i, ((da, a), (db, b)) in enumerate(zip(*out)):
+        assert da == db and (a == b).all(), f"auto exchange mode vs host loopback, chunk {i}"
+    for ov, name in ((1, "blocking"), (2, "overlapped")):
+        with pkg.Engine(4096, 4096, rule=pkg.CONWAY, device=0, rank=1, nranks=4,
+                        uid=pkg.unique_id(), exchange_overlap=ov) as e:
+            assert e.exchange == (name, 0.0, 0.0)
+
+
 def test_rccl_self_loop_two_communicators(pkg, monkeypatch):
     """A second engine on another self-loop communicator in the same process, and
     destroy/re-create: communicators are per engine."""

@@ -141,7 +141,7 @@ def main():
             print(json.dumps({"lib": os.path.basename(os.environ.get("GOL_LIB", "libgol.so")), "size": n, "nranks": N, "rank": rank, "own_rows": e.rows,
                               "halo_depth": e.halo_depth, "tb_depth": e.tb_depth,
                               "rows_per_wave": e.rows_per_wave, "handoff": e.handoff,
-                              "age_skew": e.age_skew, "skew_cfg": sk[0], "overlap_cfg": sk[1],
+                              "age_skew": e.age_skew, "skew_cfg": sk[0], "overlap_cfg": sk[1], "exchange": list(e.exchange),
                               "transport": sk[2], "shrink_cfg": sk[3], "passes": e.passes,
                               **({a.env_var: sk[4]} if a.env_var else {}),
                               "autotune": list(e.tuning),
