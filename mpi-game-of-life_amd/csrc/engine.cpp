@@ -1120,7 +1120,12 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     if (st != GOL_OK) return st;
     const uint64_t minR = h / (uint64_t)nranks;
     if (minR == 0) return fail(GOL_EINVAL, "fewer rows than ranks");
-    g->K = auto_layout(g->R, cfg).K;
+    // Depth and halo depth from the smallest stripe, which every rank computes
+    // alike: balanced stripes differ by one row, and a rank of 6145 rows beside
+    // ranks of 6144 (or 16384 beside 16383) would otherwise pick another K or Hx
+    // than its neighbours, whose exchanges then move different row counts (r07 fix;
+    // tests/test_planner.py::test_rank_geometry_agrees_across_ranks).
+    g->K = auto_layout(minR, cfg).K;
     // Rounds of halo_depth generations between exchanges: 8 launches (r03, with
     // shrinking regions: 16 for K = 16 stripes of at most 12288 rows).  Per-rank
     // proxy over the RCCL byte mover
@@ -1142,8 +1147,8 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // (profiles/r04/rank_proxy_rccl_halo_depth_sweep.jsonl); the 8-way rank keeps 8
     // (64 / 96 / 128 / 160: 106.2 / 108.3 / 109.6 / 107.9).
     const uint64_t launches_per_round =
-        shrinking ? ((g->K >= 16 && g->R <= 12288) ? 16 : 8)
-                  : ((g->K >= 16 && g->R >= 16384) ? 12 : 8);
+        shrinking ? ((g->K >= 16 && minR <= 12288) ? 16 : 8)
+                  : ((g->K >= 16 && minR >= 16384) ? 12 : 8);
     uint64_t Hx = cfg->halo_depth ? cfg->halo_depth : launches_per_round * (uint64_t)g->K;
     if (Hx > minR) Hx = minR;  // a rank sends its first/last Hx own rows
     g->Hx = nranks > 1 ? Hx : 0;

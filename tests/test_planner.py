@@ -189,3 +189,17 @@ def test_multipass_plans(pkg, monkeypatch, passes, h, rank, n):
     assert pkg.plan_model(h, 65536, rank=rank, nranks=n, tb_depth=8)["passes"] == 1
     monkeypatch.delenv("GOL_DEV_PASSES")
     assert pkg.plan_model(h, 65536, rank=rank, nranks=n, tb_depth=16)["passes"] == 1
+
+
+@pytest.mark.parametrize("h,n", [(32767, 2), (12289, 2), (65535, 4), (49151, 3), (24577, 4),
+                                 (65536, 8), (1200, 3)])
+def test_rank_geometry_agrees_across_ranks(pkg, h, n):
+    """Every rank of a split must run the same fused depth K and halo depth Hx:
+    neighbours exchange Hx rows each way per round, so a rank of 6145 rows beside
+    ranks of 6144 (K 16 vs 8) or of 16384 beside 16383 (Hx 192 vs 128) would send
+    and expect different row counts (engine.cpp rank_geometry decides both from the
+    smallest stripe, r07).  The schedules then agree op for op."""
+    got = [pkg.round_schedule(h, 4096, r, n, 300) for r in range(n)]
+    assert len({(K, Hx) for _, K, Hx in got}) == 1, [(K, Hx) for _, K, Hx in got]
+    kinds = [[(o["kind"], o["depth"]) for o in ops] for ops, _, _ in got]
+    assert all(k == kinds[0] for k in kinds)
