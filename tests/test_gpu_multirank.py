@@ -144,6 +144,21 @@ def test_group_overlap_uneven_stripes(pkg, oracle):
         assert (grp.store_packed() == oracle.bp_run(g, w, 48, oracle.CONWAY)).all()
 
 
+@pytest.mark.parametrize("h,n", [(12289, 2), (32767, 2)])
+def test_group_stripes_straddling_depth_thresholds(pkg, oracle, h, n):
+    """Auto depth and halo depth with stripes one row apart across a threshold
+    (6145 / 6144 rows: K 16 vs 8 if decided per stripe; 16384 / 16383: Hx 192 vs
+    128): every member runs the smallest stripe's K and Hx (engine.cpp
+    rank_geometry, r07), and the group equals the single field (oracle)."""
+    w, gens = 1024, 3 * 192 + 21
+    g = oracle.bp_random(h, w, 9)
+    with pkg.Group(h, w, n, rule=pkg.CONWAY) as grp:
+        assert len({(m.tb_depth, m.halo_depth) for m in grp.members}) == 1
+        grp.load_packed(g)
+        grp.step(gens)
+        assert (grp.store_packed() == oracle.bp_run(g, w, gens, oracle.CONWAY)).all()
+
+
 @pytest.mark.parametrize("kind", ["group", "composite"])
 def test_store_and_digest_without_sync_after_overlap(pkg, oracle, kind):
     """The last launch of an overlapped round writes the band rows on a second
