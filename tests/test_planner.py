@@ -203,3 +203,20 @@ def test_rank_geometry_agrees_across_ranks(pkg, h, n):
     assert len({(K, Hx) for _, K, Hx in got}) == 1, [(K, Hx) for _, K, Hx in got]
     kinds = [[(o["kind"], o["depth"]) for o in ops] for ops, _, _ in got]
     assert all(k == kinds[0] for k in kinds)
+
+
+def test_rank_geometry_agrees_sweep(pkg):
+    """The same over seeded random heights around every threshold (K at 6144 rows,
+    Hx at 16384) and every split of 2..8 ranks, plus the halo's cap (<= the
+    smallest stripe) for short stripes."""
+    import random
+    rnd = random.Random(7)
+    hs = [rnd.randrange(n * t - 3 * n, n * t + 3 * n) for t in (6144, 16384) for n in range(2, 9)]
+    hs += [rnd.randrange(16, 4000) for _ in range(12)]
+    for h in hs:
+        for n in range(2, 9):
+            if h < n:
+                continue
+            kh = {pkg.round_schedule(h, 640, r, n, 50)[1:] for r in range(n)}
+            assert len(kh) == 1, (h, n, kh)
+            assert next(iter(kh))[1] <= h // n, (h, n, kh)
