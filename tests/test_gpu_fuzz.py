@@ -1,0 +1,105 @@
+"""Seeded differential sweep (r07): random small fields through random engine
+configurations -- single engines (streaming or resident, any depth, block kind,
+strip width, rows per wavefront, REF_STRIPES), in-process groups of 2-5 stripes
+(halo depth, exchange mode), and several gol_step calls per case -- each against
+the oracle (Parallel_Life_MPI.cpp countNeighbours :16-35 + updateGrid :37-54 on
+the field, or on :70-81's stripes for REF_STRIPES).  The targeted tests pin each
+knob on chosen shapes; this sweep crosses them on shapes nobody chose.  A
+configuration the engine rejects (GOL_EINVAL: e.g. a depth too small for hand-off
+blocks) must be rejected up front, never produce a wrong field.
+"""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DEPTHS = [0, 1, 2, 4, 6, 7, 8, 12, 16]
+RULES = {
+    "ref": (0, 1 << 2),
+    "conway": (1 << 3, (1 << 2) | (1 << 3)),
+    "highlife": ((1 << 3) | (1 << 6), (1 << 2) | (1 << 3)),
+    "seeds": (1 << 2, 0),
+    "daynight": ((1 << 3) | (1 << 6) | (1 << 7) | (1 << 8),
+                 (1 << 3) | (1 << 4) | (1 << 6) | (1 << 7) | (1 << 8)),
+    "b0": ((1 << 0) | (1 << 3), (1 << 2) | (1 << 3)),
+}
+
+
+def draw(rnd):
+    """One random case: shape, rule, knobs, and the generation chunks of its steps."""
+    h = rnd.choice([rnd.randint(1, 40), rnd.randint(41, 400), rnd.randint(401, 1500),
+                    rnd.randint(1501, 5000)])
+    w = rnd.choice([rnd.randint(1, 70), rnd.randint(71, 1000), rnd.randint(1001, 5000),
+                    rnd.randint(5001, 9000)])
+    rule = rnd.choice(sorted(RULES))
+    kind = rnd.choice(["single", "single", "single", "ref_stripes", "group"])
+    knobs = dict(tb_depth=rnd.choice(DEPTHS))
+    if rnd.random() < 0.4:
+        knobs["handoff"] = rnd.choice([1, 2])
+    if rnd.random() < 0.3:
+        knobs["strip_lanes"] = rnd.choice([64, 32, 16])
+    if rnd.random() < 0.3:
+        knobs["rows_per_wave"] = rnd.randint(1, 120)
+    if kind == "single" and rnd.random() < 0.3:
+        knobs = dict(resident=2, tb_depth=rnd.choice([0, 1, 3, 8, 16, 21]),
+                     rows_per_wave=rnd.choice([0, 2, 3, 4, 6, 8]))
+    elif kind == "single" and rnd.random() < 0.15:
+        knobs["streams"] = rnd.choice([2, 3])  # the composite engine (stripes on streams)
+    n = 1
+    if kind == "group":
+        n = rnd.randint(2, 5)
+        if rnd.random() < 0.5:
+            knobs["halo_depth"] = rnd.randint(1, 64)
+        knobs["exchange_overlap"] = rnd.choice([0, 1, 2])
+    P = rnd.randint(1, 6) if kind == "ref_stripes" else 1
+    chunks = [rnd.choice([0, 1, 2, 3, 5, 16, 17, rnd.randint(1, 90)]) for _ in range(rnd.randint(1, 3))]
+    return dict(h=h, w=w, rule=rule, kind=kind, n=n, P=P, knobs=knobs, chunks=chunks,
+                seed=rnd.randint(1, 1 << 30))
+
+
+def expected(oracle, g, case, gens):
+    R = RULES[case["rule"]]
+    if case["kind"] == "ref_stripes" and case["P"] > 1:
+        return oracle.bp_ref_stripes(g, case["w"], gens, case["P"], R)
+    return oracle.bp_run(g, case["w"], gens, R)
+
+
+@pytest.mark.parametrize("block", range(8))
+def test_random_configurations_vs_oracle(pkg, oracle, block):
+    rnd = random.Random(20261018 + block)
+    ran = rejected = 0
+    for i in range(60):
+        case = draw(rnd)
+        h, w = case["h"], case["w"]
+        if case["kind"] == "group" and h < case["n"]:
+            continue
+        if case["kind"] == "ref_stripes" and h < case["P"]:
+            continue
+        g = oracle.bp_random(h, w, case["seed"])
+        R = RULES[case["rule"]]
+        try:
+            if case["kind"] == "group":
+                eng = pkg.Group(h, w, case["n"], rule=R, **case["knobs"])
+            else:
+                sem = pkg.SEM_REF_STRIPES if case["kind"] == "ref_stripes" else pkg.SEM_GLOBAL
+                eng = pkg.Engine(h, w, rule=R, device=0, semantics=sem, ref_ranks=case["P"],
+                                 **case["knobs"])
+        except pkg.GolError as ex:
+            assert ex.status == pkg.GOL_EINVAL, (case, ex)
+            rejected += 1
+            continue
+        with eng:
+            eng.load_packed(g)
+            done = 0
+            for c in case["chunks"]:
+                eng.step(c)
+                done += c
+                want = expected(oracle, g, case, done)
+                got = eng.store_packed()
+                assert got.shape == want.shape, case
+                assert (got == want).all(), f"case {block}.{i} after {done} generations: {case}"
+                assert eng.digest() == oracle.bp_digest(want, w), case
+        ran += 1
+    assert ran >= 40, (ran, rejected)
+    print(f"block {block}: {ran} configurations run, {rejected} rejected up front")
