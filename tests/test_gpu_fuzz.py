@@ -10,6 +10,7 @@ blocks) must be rejected up front, never produce a wrong field.
 """
 import random
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -103,3 +104,64 @@ def test_random_configurations_vs_oracle(pkg, oracle, block):
         ran += 1
     assert ran >= 40, (ran, rejected)
     print(f"block {block}: {ran} configurations run, {rejected} rejected up front")
+
+
+def mirrored_steps(oracle, own, w, chunks, rule, Hx, has_up, has_dn):
+    """A rank whose transport returns what it is sent: each round its halos hold
+    its own first / last Hx rows, the extended stripe evolves with dead cells
+    beyond it, and its own rows are kept (as tests/test_gpu_rccl.py); every
+    gol_step call starts a round, rounds are Hx generations."""
+    outs = []
+    for c in chunks:
+        left = c
+        while left:
+            g = min(left, Hx)
+            parts = ([own[:Hx]] if has_up else []) + [own] + ([own[-Hx:]] if has_dn else [])
+            ext = oracle.bp_run(np.concatenate(parts), w, g, rule)
+            top = Hx if has_up else 0
+            own = ext[top:top + own.shape[0]]
+            left -= g
+        outs.append(own)
+    return outs
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_random_rank_engines_vs_oracle(pkg, oracle, block):
+    """Rank engines (gol_create_rank_transport) of random splits with a loopback
+    transport: random rank of 2-8, depth, halo depth, exchange mode, block kind and
+    step chunks, against the oracle evolving the mirrored extended stripe."""
+    rnd = random.Random(7100 + block)
+    ran = 0
+    for i in range(20):
+        n = rnd.randint(2, 8)
+        h = rnd.randint(2 * n, 3000)
+        w = rnd.randint(1, 6000)
+        rule = rnd.choice(sorted(RULES))
+        R = RULES[rule]
+        rank = rnd.randrange(n)
+        knobs = dict(tb_depth=rnd.choice(DEPTHS), exchange_overlap=rnd.choice([0, 1, 2]))
+        if rnd.random() < 0.5:
+            knobs["halo_depth"] = rnd.randint(1, 80)
+        if rnd.random() < 0.3:
+            knobs["handoff"] = rnd.choice([1, 2])
+        chunks = [rnd.choice([1, 5, 16, rnd.randint(1, 150)]) for _ in range(rnd.randint(1, 3))]
+        g = oracle.bp_random(h, w, rnd.randint(1, 1 << 30))
+        try:
+            e = pkg.Engine(h, w, rule=R, device=0, rank=rank, nranks=n,
+                           transport=lambda su, sd: (su, sd), **knobs)
+        except pkg.GolError as ex:
+            assert ex.status == pkg.GOL_EINVAL, (ex, knobs)
+            continue
+        with e:
+            own = g[e.row0:e.row0 + e.rows]
+            e.load_packed(own)
+            got = []
+            for c in chunks:
+                e.step(c)
+                got.append(e.store_packed())
+            Hx = e.halo_depth
+        want = mirrored_steps(oracle, own, w, chunks, R, Hx, rank > 0, rank < n - 1)
+        for j, (a, b) in enumerate(zip(got, want)):
+            assert (a == b).all(), f"case {block}.{i} chunk {j}: h {h} w {w} rank {rank}/{n} {rule} {knobs} {chunks}"
+        ran += 1
+    assert ran >= 12
