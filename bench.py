@@ -334,7 +334,7 @@ def rank_breakdown(eng, tm, dt, steps, rank):
         between rounds (the max-over-ranks barrier is not in it).
     avg_launch_ms: the mean sampled launch (overlapped band and interior launches
     run concurrently, so launches x mean is not a time share).  Rows per launch =
-    the buffer rows a full-depth launch computes (engine.cpp rank_geometry)."""
+    the buffer rows a full-depth launch computes (stripes.cpp rank_geometry)."""
     launches = max(tm["launches"], 1)
     avg = tm["kernel_ms"] / launches
     span = tm["round_ms"] / steps
@@ -404,7 +404,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # GOL_DEV_RCCL_SELF=1 (rehearsal of the N > 1 path on a one-GPU box): every
-    # rank's engine talks RCCL to itself (engine.cpp gol_create_rank), ranks share
+    # rank's engine talks RCCL to itself (stripes.cpp gol_create_rank), ranks share
     # the GPUs there are, torch.distributed runs over gloo (RCCL refuses two ranks
     # of one communicator on one device), and rccl_selfcheck is expected to fail
     # (a self-looped stripe is not the field's stripe).  Such a record carries
@@ -561,7 +561,7 @@ def main():
                 "columns": list(eng.columns),
                 # the plan the timed launches ran: the cost models' plan or the
                 # autotuner's variant, with the create-time best launch (us) of
-                # each (engine.cpp autotune_plans; rank 0's first full-depth plan)
+                # each (plan.cpp autotune_plans; rank 0's first full-depth plan)
                 "autotune": {"variant": tuning[0], "launch_us": tuning[1],
                              "models_launch_us": tuning[2],
                              "gain": (round(tuning[2] / tuning[1] - 1, 4)

@@ -39,7 +39,7 @@ EXPORTS = [
     "gol_plan_resident_rows", "gol_plan_exchange",
 ]
 
-# gol_plan_tuning's variants (engine.cpp kTuneVariantNames): 0 = the models' plan
+# gol_plan_tuning's variants (plan.cpp kTuneVariantNames): 0 = the models' plan
 TUNE_VARIANTS = ["models", "no_half_strip", "skew_0.95", "skew_1.05", "other_block_kind"]
 
 

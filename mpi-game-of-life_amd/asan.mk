@@ -1,5 +1,6 @@
 # Host sanitizer build ("Host ASan/UBSan in CPU tests"): the host
-# code of libgol.so (engine.cpp: planner, schedule, partition and config logic)
+# code of libgol.so (engine.cpp, plan.cpp, stripes.cpp: planner, schedule, partition
+# and config logic)
 # under AddressSanitizer + UndefinedBehaviorSanitizer, linked with the regular
 # gfx950 kernel objects (device code is never sanitized: GPU ASan does not exist
 # on this pool).  CPU only -- tools/asan_cpu_suite.sh runs the CPU test suite
@@ -9,11 +10,11 @@ include Makefile
 LLVM ?= $(ROCM)/lib/llvm/bin
 ASAN_HOST = -O1 -g -fno-omit-frame-pointer -Xarch_host -fsanitize=address \
 	-Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined
-ASAN_OBJ = $(filter-out build/engine.o,$(OBJ)) build/asan/engine.o
+ASAN_OBJ = $(filter-out $(foreach u,$(HOST),build/$(u).o),$(OBJ)) $(foreach u,$(HOST),build/asan/$(u).o)
 
 asan: build/asan/libgol_asan.so
 
-build/asan/engine.o: csrc/engine.cpp $(HDR)
+build/asan/%.o: csrc/%.cpp $(HDR)
 	@mkdir -p build/asan
 	$(HIPCC) -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter $(ASAN_HOST) -c -o $@ $<
 

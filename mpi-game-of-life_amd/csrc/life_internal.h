@@ -86,7 +86,7 @@ struct StepArgs {
     int64_t side_slot;    // words per slot: 2 (K-1) rows x 64 lanes x NP/2 words
     uint64_t* wlog;       // dev timing builds only (GOL_EXP & 128): 8 words per wavefront
     uint32_t* prog;       // dev (GOL_EXP & 1024): per-SIMD wave progress, 2 words per SIMD
-    // Edge-aligned strips and the packed half strip (engine.cpp col_layout;
+    // Edge-aligned strips and the packed half strip (plan.cpp col_layout;
     // one-segment launches of 64-lane strips).  A lane whose neighbour lane is the
     // DPP shift's zero (lane 0 / 63) or outside the field is exact, so strip 0 starts
     // at group 0 (63 output groups), strip s at group 62 s (lane 0 its halo), and

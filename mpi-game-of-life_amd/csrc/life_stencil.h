@@ -533,7 +533,7 @@ void life_tb_kernel(StepArgs a)
     // their segment from the kernel arguments, which arrive with the first scalar
     // loads, instead of a dependent table walk in memory at every wavefront's
     // start; the half strip's units use it with one block from pair0 (the device
-    // table's extra segment, engine.cpp build_plans).
+    // table's extra segment, plan.cpp build_plans).
     SegDesc sg;
     if (a.seg0_only) {
         sg = a.seg0;

@@ -9,7 +9,7 @@ if ROOT not in sys.path:
 
 import __graft_entry__ as entry  # noqa: E402
 
-# The engine's autotuner (engine.cpp autotune_plans) times a few variants of the
+# The engine's autotuner (plan.cpp autotune_plans) times a few variants of the
 # cost models' plan at create and may pick another, equally exact one.  Parity
 # tests run with it on (the shipped default); tests that pin plan properties (the
 # skew lengths, the half strip's layout, the waiting-kernel registry's block

@@ -7,7 +7,7 @@ partition, the rounds of Hx generations, the launch depths, the shrinking output
 rows, the band/interior split and the overlapped exchange) and executes it on a
 bool field with numpy: a launch of depth d writes ONLY its scheduled output rows
 (every other row of the target buffer is filled with noise), exchanges move the
-Hx boundary rows with torch.distributed send/recv as engine.cpp `exchange` does.
+Hx boundary rows with torch.distributed send/recv as stripes.cpp `exchange` does.
 A schedule that reads a row nobody computed, or a round/exchange order change
 that breaks the protocol, shows up as a mismatch with the oracle.
 """
@@ -51,7 +51,7 @@ def run_launch(cur, nxt, depth, segs, rule, glob0, field_h):
 
 
 def exchange(buf, rank, world, R, Hx):
-    """engine.cpp `exchange`: own rows [Hx, 2Hx) up and [R, R+Hx) down, received
+    """stripes.cpp `exchange`: own rows [Hx, 2Hx) up and [R, R+Hx) down, received
     into [0, Hx) and [R+Hx, R+2Hx)."""
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.uint8))
     w = buf.shape[1]
@@ -163,7 +163,7 @@ def test_rank_protocol_from_engine_schedule(oracle, monkeypatch, world, K, Hx, c
 
 
 def test_default_halo_depth(pkg, monkeypatch):
-    """Rounds of 8 launches, 12 for K = 16 stripes of 16384+ rows (engine.cpp
+    """Rounds of 8 launches, 12 for K = 16 stripes of 16384+ rows (stripes.cpp
     rank_geometry: the round's full-depth launches share one region, so deeper
     halos cost rows on every launch); with the
     r03 shrinking regions (GOL_DEV_RANK_SHRINK=1) 16 for K = 16 stripes of at most

@@ -1,4 +1,4 @@
-"""GPU parity of autotuned plans (engine.cpp build_plans variants +
+"""GPU parity of autotuned plans (plan.cpp build_plans variants +
 autotune_plans).
 
 At create, an engine alone on its device times the cost models' plan of every

@@ -1,7 +1,7 @@
 """GPU parity at the benchmark sizes (BASELINE.json configs[2..4]).
 
 The timed path itself: gol_create(65536, 65536) with defaults is one stream of
-K = 16 launches with age-skewed row blocks (engine.cpp age_skew) -- exactly what
+K = 16 launches with age-skewed row blocks (plan.cpp age_skew) -- exactly what
 bench.py measures; the 2-stripe composite engine (streams=2: 2 same-device
 stripes on 2 streams, 256-row halo rounds) is checked the same way.  Checked
   * against the CPU oracle after one step(16) call (the K = 16 kernel runs);

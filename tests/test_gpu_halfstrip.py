@@ -1,5 +1,5 @@
 """GPU parity of the edge-aligned strips and the packed half strip
-(engine.cpp col_layout / half_units, life_stencil.h).
+(plan.cpp col_layout / half_units, life_stencil.h).
 
 64-lane strips start at the field's left edge (strip 0 outputs groups 0..62: its
 lane 0 sees the DPP shift's zero, the dead border of Parallel_Life_MPI.cpp:26-27)
@@ -93,7 +93,7 @@ def test_half_strip_equals_full_strips(pkg, monkeypatch, h, w):
 @pytest.mark.parametrize("h,hand,half", [(8448, True, True), (16640, True, True),
                                          (33024, False, True), (65536, False, True)])
 def test_block_kind_policy(pkg, h, hand, half):
-    """The planner's choice per stripe height (engine.cpp build_plans,
+    """The planner's choice per stripe height (plan.cpp build_plans,
     kHalfClassicRows): hand-off blocks for short stripes, classic blocks once their
     young blocks reach 160 rows, both with the half strip
     (profiles/r03/ab_half_strip_handoff_scale_sweep.jsonl)."""

@@ -1,4 +1,4 @@
-"""GPU parity of age-skewed row blocks (engine.cpp age_skew, life_stencil.h).
+"""GPU parity of age-skewed row blocks (plan.cpp age_skew, life_stencil.h).
 
 A one-round launch at 2 wavefronts per SIMD gives the units dispatched first
 (the older wave of each SIMD) longer row blocks than the others.  The blocks of a

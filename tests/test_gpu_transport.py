@@ -7,7 +7,7 @@ schedule -- with the halo rows moved by a caller's host transport instead: here
 torch.distributed over gloo between 2-4 processes that share cuda:0 (the same
 transport shape as the reference's MPI_Sendrecv of boundary rows,
 Parallel_Life_MPI.cpp:104-145, with the receive landing in the halo).  Only the
-byte mover differs from the RCCL path (engine.cpp `exchange`).  Also the
+byte mover differs from the RCCL path (stripes.cpp `exchange`).  Also the
 `gol-mpi --transport mpi` launcher under mpirun -np 2 / 4 on one GPU.
 """
 import hashlib
@@ -80,7 +80,7 @@ def worker(rank, world, port, h, w, chunks, rule, seed, cfg, q):
 
 def run_ranks(world, h, w, chunks, rule, seed, **cfg):
     # ranks sharing one GPU: classic row blocks (one waiting launch per device at a
-    # time, engine.cpp gol_create_group)
+    # time, stripes.cpp gol_create_group)
     cfg.setdefault("handoff", 1)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

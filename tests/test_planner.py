@@ -1,4 +1,4 @@
-"""CPU suite: the launch planner (engine.cpp build_plans, pick_rows_per_wave,
+"""CPU suite: the launch planner (plan.cpp build_plans, pick_rows_per_wave,
 age_skew, col_layout, half_units, rank_geometry) through the host-only model
 gol_plan_model -- no GPU.  Also run under the host sanitizers
 (tools/asan_cpu_suite.sh).
@@ -197,7 +197,7 @@ def test_rank_geometry_agrees_across_ranks(pkg, h, n):
     """Every rank of a split must run the same fused depth K and halo depth Hx:
     neighbours exchange Hx rows each way per round, so a rank of 6145 rows beside
     ranks of 6144 (K 16 vs 8) or of 16384 beside 16383 (Hx 192 vs 128) would send
-    and expect different row counts (engine.cpp rank_geometry decides both from the
+    and expect different row counts (stripes.cpp rank_geometry decides both from the
     smallest stripe, r07).  The schedules then agree op for op."""
     got = [pkg.round_schedule(h, 4096, r, n, 300) for r in range(n)]
     assert len({(K, Hx) for _, K, Hx in got}) == 1, [(K, Hx) for _, K, Hx in got]

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of age-skewed row blocks (engine.cpp age_skew) in ONE process, interleaved
+"""A/B of age-skewed row blocks (plan.cpp age_skew) in ONE process, interleaved
 rounds: single-stream engines of the per-GPU stripe shapes built with
 GOL_DEV_AGE_SKEW = each value of --rhos (0 = equal blocks), wall-clock TCUPS
 (median of the rounds), the plan, and whether every variant's field digest

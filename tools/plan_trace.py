@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Dev tool: per-plan launch durations of a rank engine (tools/rank_plans.py run
 under rocprofv3 --kernel-trace).  Launch j of every round runs the plan of its cumulative shrink,
-plans[(j+1) K - 1] (engine.cpp round_ops); prints
+plans[(j+1) K - 1] (stripes.cpp round_ops); prints
 per plan: rows, blocks kind and lengths, mean duration, and the rate per row.
 
     python tools/plan_trace.py gpurun_out/r03n/t256 gpurun_out/r03n/plans256.err gpurun_out/r03n/plans256.json
