@@ -165,3 +165,31 @@ def test_random_rank_engines_vs_oracle(pkg, oracle, block):
             assert (a == b).all(), f"case {block}.{i} chunk {j}: h {h} w {w} rank {rank}/{n} {rule} {knobs} {chunks}"
         ran += 1
     assert ran >= 12
+
+
+@pytest.mark.parametrize("block", range(2))
+def test_random_ascii_round_trips(pkg, oracle, block):
+    """The GPU ASCII codec (readGridFromFile's parse :91-99 and writeDataToFile's
+    serialisation :157-164) on random shapes: data.txt bytes of a random field load
+    to the oracle's packing, step, and store back as the oracle's bytes; a field
+    of REF_STRIPES engines likewise (its output keeps each stripe's own rows)."""
+    rnd = random.Random(515 + block)
+    for _ in range(12):
+        h, w = rnd.randint(1, 900), rnd.randint(1, 3000)
+        g = oracle.bp_random(h, w, rnd.randint(1, 1 << 30))
+        data = oracle.bp_unpack(g, w)
+        assert len(data) == h * (w + 1)
+        P = rnd.randint(1, 5) if h >= 5 else 1
+        sem = pkg.SEM_REF_STRIPES if P > 1 else pkg.SEM_GLOBAL
+        gens = rnd.choice([0, 1, 7, 33])
+        with pkg.Engine(h, w, device=0, semantics=sem, ref_ranks=P) as e:
+            e.load_ascii(data)
+            assert (e.store_packed() == g).all()
+            e.step(gens)
+            out = e.store_ascii(h * (w + 1))
+        if h * w <= 200000:  # the scalar restatement of the whole program
+            want = oracle.ref_program(data, h, w, gens, P)
+        else:
+            kind = "ref_stripes" if P > 1 else "single"
+            want = oracle.bp_unpack(expected(oracle, g, dict(kind=kind, P=P, w=w, rule="ref"), gens), w)
+        assert out == want, (h, w, P, gens)
