@@ -8,12 +8,15 @@ knob on chosen shapes; this sweep crosses them on shapes nobody chose.  A
 configuration the engine rejects (GOL_EINVAL: e.g. a depth too small for hand-off
 blocks) must be rejected up front, never produce a wrong field.
 """
+import os
 import random
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+# GOL_FUZZ_SCALE=n runs n times the seeds (a longer sweep by hand; default 1)
+SCALE = max(1, int(os.environ.get("GOL_FUZZ_SCALE", "1")))
 
 DEPTHS = [0, 1, 2, 4, 6, 7, 8, 12, 16]
 RULES = {
@@ -66,7 +69,7 @@ def expected(oracle, g, case, gens):
     return oracle.bp_run(g, case["w"], gens, R)
 
 
-@pytest.mark.parametrize("block", range(8))
+@pytest.mark.parametrize("block", range(8 * SCALE))
 def test_random_configurations_vs_oracle(pkg, oracle, block):
     rnd = random.Random(20261018 + block)
     ran = rejected = 0
@@ -125,7 +128,7 @@ def mirrored_steps(oracle, own, w, chunks, rule, Hx, has_up, has_dn):
     return outs
 
 
-@pytest.mark.parametrize("block", range(4))
+@pytest.mark.parametrize("block", range(4 * SCALE))
 def test_random_rank_engines_vs_oracle(pkg, oracle, block):
     """Rank engines (gol_create_rank_transport) of random splits with a loopback
     transport: random rank of 2-8, depth, halo depth, exchange mode, block kind and
@@ -167,7 +170,7 @@ def test_random_rank_engines_vs_oracle(pkg, oracle, block):
     assert ran >= 12
 
 
-@pytest.mark.parametrize("block", range(2))
+@pytest.mark.parametrize("block", range(2 * SCALE))
 def test_random_ascii_round_trips(pkg, oracle, block):
     """The GPU ASCII codec (readGridFromFile's parse :91-99 and writeDataToFile's
     serialisation :157-164) on random shapes: data.txt bytes of a random field load

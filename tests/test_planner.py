@@ -136,6 +136,24 @@ def test_single_field_plans_sweep(pkg, seed):
         check_plan(p)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_rank_plans_sweep(pkg, seed):
+    """Random splits (2-16 ranks, any rank, uneven stripes, both rules, both
+    exchange modes): every rank's first full-depth plan tiles its rows and keeps
+    the kernel's invariants."""
+    import random
+    rnd = random.Random(100 + seed)
+    for _ in range(30):
+        n = rnd.randint(2, 16)
+        h = rnd.choice([rnd.randint(2 * n, 3000), rnd.randint(3000, 70000), rnd.randint(70000, 270000)])
+        w = rnd.choice([rnd.randint(1, 4200), rnd.randint(4200, 70000), 65536])
+        rank = rnd.randrange(n)
+        rule = rnd.choice([pkg.REF_RULE, pkg.CONWAY])
+        p = pkg.plan_model(h, w, rank=rank, nranks=n, rule=rule,
+                           exchange_overlap=rnd.choice([0, 1, 2]))
+        check_plan(p)
+
+
 @pytest.mark.parametrize("h", [8192 + 2 * 128, 12288, 16384 + 2 * 192, 33024, 40000])
 @pytest.mark.parametrize("handoff", [0, 1, 2])
 def test_block_kinds_and_forced_lengths(pkg, h, handoff):
