@@ -459,7 +459,7 @@ def main():
         # side stream beside the interior launch, exchange_overlap = 2) and blocking
         # (after the round's last launch, 1) -- over the same K steps, reported beside
         # `value`, which is the default engine's: exchange_overlap = 0, the mode the
-        # engine chose at create by timing both on this communicator (r07)
+        # engine chose at create by timing both on this communicator (late r06)
         modes = {}
         for name, ov in (("overlapped", 2), ("blocking", 1)):
             eng = rank_engine(ov)
@@ -554,7 +554,7 @@ def main():
                 "tb_depth": eng.tb_depth, "word_planes": eng.word_planes,
                 "halo_depth": eng.halo_depth, "rows_per_wave": eng.rows_per_wave,
                 "handoff": eng.handoff, "resident": eng.resident,
-                # N > 1: the exchange mode the rank engines chose at create (r07)
+                # N > 1: the exchange mode the rank engines chose at create (late r06)
                 "exchange": eng.exchange[0] if world > 1 else None,
                 "age_skew": eng.age_skew,
                 # (strips per row block, half-strip wavefronts, half-strip lane groups)

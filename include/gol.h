@@ -258,7 +258,7 @@ gol_status gol_plan_resident(gol_engine* e, uint32_t* on, uint32_t* bands, uint3
  * the models' plan (0 when nothing was timed).  Out pointers may be NULL. */
 gol_status gol_plan_tuning(gol_engine* e, uint32_t* variant, float* tuned_us, float* model_us);
 
-/* (r07) Exchange mode of a stripe engine: *mode = 1 blocking (the exchange after
+/* (late r06) Exchange mode of a stripe engine: *mode = 1 blocking (the exchange after
  * the round's last launch), 2 overlapped (band launch, then the exchange beside
  * the interior launch), 0 for an engine without halo exchanges.  With
  * exchange_overlap = 0 a rank engine over RCCL chooses it at create by timing

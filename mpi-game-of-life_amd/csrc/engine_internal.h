@@ -230,7 +230,7 @@ struct gol_engine {
     bool overlap = false;     // the mode gol_step runs (RankGeom::overlap at create)
     bool band_plans = false;  // the band and interior plans exist (RankGeom::band)
     bool halo_fresh = false;
-    // (r07) exchange_overlap = 0 on a rank engine over RCCL: both modes timed at
+    // (late r06) exchange_overlap = 0 on a rank engine over RCCL: both modes timed at
     // create (tune_exchange), the max over ranks of each mode's best sample (ms);
     // 0 = not timed
     bool xchg_tune = false;

@@ -18,7 +18,7 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // Depth and halo depth from the smallest stripe, which every rank computes
     // alike: balanced stripes differ by one row, and a rank of 6145 rows beside
     // ranks of 6144 (or 16384 beside 16383) would otherwise pick another K or Hx
-    // than its neighbours, whose exchanges then move different row counts (r07 fix;
+    // than its neighbours, whose exchanges then move different row counts (late-r06 fix;
     // tests/test_planner.py::test_rank_geometry_agrees_across_ranks).
     g->K = auto_layout(minR, cfg).K;
     // Rounds of halo_depth generations between exchanges: 8 launches (r03, with
@@ -98,7 +98,7 @@ gol_status rank_geometry(uint64_t h, const gol_config* cfg, int rank, int nranks
     // blocking and bimodal at 2 ranks, and an RCCL exchange is itself a kernel that
     // needs free slots: blocking was the rank default through r06, measured on the
     // RCCL self-loop, where the exchange is a device-local copy.  Over xGMI the
-    // exchange costs more and may be worth hiding, so (r07) with
+    // exchange costs more and may be worth hiding, so (late r06) with
     // gol_config.exchange_overlap = 0 a rank engine over RCCL (tune_ok) builds both
     // schedules' plans, starts blocking, and gol_create_rank times both modes on
     // the real communicator and keeps the faster (tune_exchange).
@@ -508,7 +508,7 @@ gol_status make_rank_engine(uint64_t h, uint64_t w, const gol_config* cfg, int r
     return GOL_OK;
 }
 
-// (r07) gol_config.exchange_overlap = 0 on a rank engine over RCCL: time both
+// (late r06) gol_config.exchange_overlap = 0 on a rank engine over RCCL: time both
 // exchange modes on this communicator -- blocking (after the round's last launch)
 // and overlapped (band launch, then the exchange on the comm stream beside the
 // interior launch) -- and keep the faster.  Both schedules are bit-exact (the

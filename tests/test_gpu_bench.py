@@ -46,7 +46,7 @@ def test_bench_json_contract():
 def test_bench_two_rank_rehearsal_exchange_modes():
     """bench.py --gpus 2 under torch.distributed.run on ONE GPU (GOL_DEV_RCCL_SELF=1:
     each rank's engine talks RCCL to itself, ranks over gloo): the N > 1 record
-    carries both forced exchange modes and the default engine's own choice (r07),
+    carries both forced exchange modes and the default engine's own choice (late r06),
     and a rehearsal never reports an N-GPU value."""
     env = dict(os.environ, GOL_DEV_RCCL_SELF="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",

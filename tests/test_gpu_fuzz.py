@@ -1,4 +1,4 @@
-"""Seeded differential sweep (r07): random small fields through random engine
+"""Seeded differential sweep (late r06): random small fields through random engine
 configurations -- single engines (streaming or resident, any depth, block kind,
 strip width, rows per wavefront, REF_STRIPES), in-process groups of 2-5 stripes
 (halo depth, exchange mode), and several gol_step calls per case -- each against

@@ -149,7 +149,7 @@ def test_group_stripes_straddling_depth_thresholds(pkg, oracle, h, n):
     """Auto depth and halo depth with stripes one row apart across a threshold
     (6145 / 6144 rows: K 16 vs 8 if decided per stripe; 16384 / 16383: Hx 192 vs
     128): every member runs the smallest stripe's K and Hx (stripes.cpp
-    rank_geometry, r07), and the group equals the single field (oracle)."""
+    rank_geometry, late r06), and the group equals the single field (oracle)."""
     w, gens = 1024, 3 * 192 + 21
     g = oracle.bp_random(h, w, 9)
     with pkg.Group(h, w, n, rule=pkg.CONWAY) as grp:

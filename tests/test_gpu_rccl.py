@@ -182,7 +182,7 @@ def test_rank_timing_spans_add_up(pkg, monkeypatch, overlap):
 
 @pytest.mark.parametrize("world,rank,size", [(4, 1, 4096), (8, 3, 65536)])
 def test_rccl_exchange_mode_chosen_at_create(pkg, monkeypatch, world, rank, size):
-    """exchange_overlap = 0 (r07): a rank engine over RCCL times rounds of both
+    """exchange_overlap = 0 (late r06): a rank engine over RCCL times rounds of both
     exchange modes at create on its communicator (stripes.cpp tune_exchange; the
     self-loop here, xGMI between two MI355X) and keeps the faster.  Whichever it
     keeps, its field equals the host loopback transport's (which blocks) bytewise

@@ -216,7 +216,7 @@ def test_rank_geometry_agrees_across_ranks(pkg, h, n):
     neighbours exchange Hx rows each way per round, so a rank of 6145 rows beside
     ranks of 6144 (K 16 vs 8) or of 16384 beside 16383 (Hx 192 vs 128) would send
     and expect different row counts (stripes.cpp rank_geometry decides both from the
-    smallest stripe, r07).  The schedules then agree op for op."""
+    smallest stripe, late r06).  The schedules then agree op for op."""
     got = [pkg.round_schedule(h, 4096, r, n, 300) for r in range(n)]
     assert len({(K, Hx) for _, K, Hx in got}) == 1, [(K, Hx) for _, K, Hx in got]
     kinds = [[(o["kind"], o["depth"]) for o in ops] for ops, _, _ in got]
